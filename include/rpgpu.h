@@ -1,0 +1,250 @@
+/*
+ * rpgpu.h — C ABI of the MI355X record-batch validation / decode engine.
+ *
+ * This is the drop-in boundary for Redpanda's record-batch hot path
+ * (SURVEY.md §8b).  Every entry point is `extern "C"`, takes plain pointers
+ * and sizes, never throws and reports errors through an int32 status.
+ * The reference interfaces each entry point replaces are cited beside it
+ * (paths relative to the reference tree's src/v/).
+ *
+ * Layouts used throughout
+ *   - Kafka v2 wire batch, big-endian 61-byte header
+ *       (kafka/protocol/kafka_batch_adapter.h:26-38, kafka/protocol/wire.h:645-681)
+ *   - Redpanda on-disk batch, little-endian 61-byte header
+ *       (storage/parser.cc:40-80, storage/segment_appender_utils.cc:28-51)
+ *
+ * An "arena" is one device (or pinned host) buffer holding many batches back
+ * to back plus an array of rpgpu_batch_desc, one per batch.  The data buffer
+ * must stay readable for RPGPU_ARENA_TAIL_PAD bytes past the last batch: the
+ * kernels read headers as whole 64-byte windows and mask what lies beyond.
+ */
+#ifndef RPGPU_H
+#define RPGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RPGPU_ABI_VERSION 1
+#define RPGPU_ARENA_TAIL_PAD 64
+#define RPGPU_HEADER_SIZE 61 /* model/record.h:527-540 */
+
+/* ---- status codes (return values) ------------------------------------- */
+enum rpgpu_status {
+    RPGPU_OK = 0,
+    RPGPU_PENDING = 1,
+    RPGPU_EINVAL = -1,
+    RPGPU_ENOMEM = -2,
+    RPGPU_EDEVICE = -3, /* HIP runtime error; see rpgpu_last_error() */
+    RPGPU_ECAPACITY = -4, /* an output buffer is too small */
+};
+
+/* ---- batch formats and operations ------------------------------------- */
+enum rpgpu_format {
+    RPGPU_FMT_KAFKA_WIRE = 0, /* produce path: kafka_batch_adapter::adapt */
+    RPGPU_FMT_RP_DISK = 1,    /* storage path: continuous_batch_parser     */
+};
+
+enum rpgpu_op {
+    RPGPU_OP_CRC = 1u << 0,    /* Kafka CRC32C over the batch body        */
+    RPGPU_OP_HDRCRC = 1u << 1, /* internal_header_only_crc                */
+    RPGPU_OP_PARSE = 1u << 2,  /* record field walk (uncompressed batches)*/
+    RPGPU_OP_INDEX = 1u << 3,  /* emit per-record index entries           */
+    RPGPU_OP_DECOMP = 1u << 4, /* decompress compressed bodies            */
+};
+#define RPGPU_OPS_PRODUCE (RPGPU_OP_CRC | RPGPU_OP_HDRCRC | RPGPU_OP_PARSE | RPGPU_OP_INDEX)
+
+/* ---- per-batch verdicts ------------------------------------------------
+ * Produce path, built from kafka_batch_adapter.cc:136-198,
+ * model/record.h:283-300,668-691, model/record_utils.cc:93-176 and
+ * kafka/server/handlers/produce.cc:440-489.  SURVEY.md §8a verdict table.
+ */
+enum rpgpu_verdict {
+    RPGPU_V_OK = 0,
+    RPGPU_V_NULL_RECORDS = 1,      /* records field null (produce.cc:440-449)      */
+    RPGPU_V_TOO_SMALL = 2,         /* < 12 bytes: adapter flags indeterminate     */
+    RPGPU_V_HDR_TRUNC_THROW = 3,   /* out_of_range escapes read_header            */
+    RPGPU_V_BAD_MAGIC = 4,         /* magic != 2 -> !v2_format                     */
+    RPGPU_V_CRC_MISMATCH = 5,      /* !valid_crc -> corrupt_message                */
+    RPGPU_V_BAD_CODEC_THROW = 6,   /* attrs codec 5..7: runtime_error escapes      */
+    RPGPU_V_BODY_TRUNC_THROW = 7,  /* parser.share(size-61) skip throws            */
+    RPGPU_V_REC_ATTR_EOF = 8,      /* record attrs consume_type at end of body    */
+    RPGPU_V_REC_TRAILING = 9,      /* "Record iteration stopped with N bytes ..."  */
+    RPGPU_V_REC_HCOUNT_NEG = 10,   /* headers.reserve(negative) -> length_error    */
+    RPGPU_V_REC_UNDEFINED = 11,    /* reference UB / allocation-dependent */
+    /* storage path (parser_errc, storage/parser_errc.h:18-25) */
+    RPGPU_V_HDR_CRC_MISMATCH = 20, /* parser_errc::header_only_crc_missmatch       */
+    RPGPU_V_STREAM_SHORT = 21,     /* parser_errc::input_stream_not_enough_bytes   */
+    RPGPU_V_FALLOCATED_ZERO = 22,  /* parser_errc::fallocated_file_read_zero_bytes_for_header */
+    /* decompression (compression/compression.cc:35-55 and the codec wrappers) */
+    RPGPU_V_DECOMP_ERROR = 30,     /* codec library error -> runtime_error         */
+    RPGPU_V_DECOMP_BAD_ALLOC = 31, /* zstd window > workspace -> std::bad_alloc   */
+    RPGPU_V_LZ4_TRAILING = 32,     /* unconsumed input after LZ4 frame end        */
+    RPGPU_V_DECOMP_UNSUPPORTED = 33,/* codec not implemented on this engine (gzip) */
+    RPGPU_V_DECOMP_OVERFLOW = 34,  /* decompressed size exceeds the output slot   */
+};
+
+/* Produce-path mapping of verdicts to Kafka error codes
+ * (kafka/protocol/errors.h:29,47,227). */
+#define RPGPU_KAFKA_ERR_NONE 0
+#define RPGPU_KAFKA_ERR_CORRUPT_MESSAGE 2
+#define RPGPU_KAFKA_ERR_INVALID_RECORD 87
+
+/* ---- descriptors and results ------------------------------------------ */
+typedef struct rpgpu_batch_desc {
+    uint64_t offset;    /* byte offset of the batch in the arena data buffer */
+    uint32_t length;    /* bytes of record data handed over for this batch   */
+    uint32_t partition; /* topic-partition id (sharding key)                 */
+    uint8_t format;     /* enum rpgpu_format                                 */
+    uint8_t ops;        /* enum rpgpu_op bitmask                             */
+    uint16_t flags;     /* reserved, 0                                       */
+    uint32_t reserved;  /* reserved, 0                                       */
+} rpgpu_batch_desc;     /* 24 bytes */
+
+typedef struct rpgpu_batch_result {
+    int32_t verdict;           /* enum rpgpu_verdict                            */
+    uint32_t crc;              /* computed Kafka CRC32C (record_utils.cc:82-87) */
+    uint32_t crc_expected;     /* header crc field                               */
+    uint32_t header_crc;       /* internal_header_only_crc (record_utils.cc:34-55) */
+    int32_t size_bytes;        /* RP size_bytes = batch_length + 12             */
+    int32_t record_count;
+    int64_t base_offset;
+    int32_t last_offset_delta;
+    int16_t attrs;
+    uint8_t codec;             /* attrs & 7                                     */
+    uint8_t type;              /* record_batch_type (raft_data=1 on produce)   */
+    int64_t first_timestamp;
+    int64_t max_timestamp;
+    uint32_t index_first;      /* first entry of this batch in the record index */
+    uint32_t index_count;      /* records fully parsed                          */
+} rpgpu_batch_result;          /* 64 bytes */
+
+typedef struct rpgpu_record_index {
+    int64_t offset;    /* base_offset + (int32)offset_delta                   */
+    int64_t timestamp; /* first_timestamp + timestamp_delta                   */
+    uint32_t key_off;  /* byte offset of the key within the batch             */
+    int32_t key_len;   /* (int32) decoded key length; <= 0: no key bytes      */
+    uint32_t val_off;
+    int32_t val_len;
+} rpgpu_record_index;  /* 32 bytes */
+
+/* Little-endian record_batch_header image as the reference hashes it
+ * (model/record_utils.cc:34-55).  Packed: 61 bytes, same as disk. */
+#pragma pack(push, 1)
+typedef struct rpgpu_rp_header {
+    uint32_t header_crc;
+    int32_t size_bytes;
+    int64_t base_offset;
+    int8_t type;
+    int32_t crc;
+    int16_t attrs;
+    int32_t last_offset_delta;
+    int64_t first_timestamp;
+    int64_t max_timestamp;
+    int64_t producer_id;
+    int16_t producer_epoch;
+    int32_t base_sequence;
+    int32_t record_count;
+} rpgpu_rp_header;
+#pragma pack(pop)
+
+typedef struct rpgpu_opts {
+    uint32_t flags;        /* reserved, 0 */
+    uint32_t max_batches;  /* per-submission capacity hint (0 = default)   */
+    uint64_t max_arena;    /* per-submission arena bytes hint (0 = default) */
+} rpgpu_opts;
+
+typedef struct rpgpu_ctx rpgpu_ctx;
+typedef uint64_t rpgpu_ticket;
+
+/* ---- context ----------------------------------------------------------- */
+/* One context per (Seastar shard x GPU); not thread-safe per context, which
+ * matches shard-per-core ownership. */
+rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts);
+void rpgpu_close(rpgpu_ctx* ctx);
+const char* rpgpu_last_error(const rpgpu_ctx* ctx);
+int32_t rpgpu_abi_version(void);
+/* CU count of the device and the persistent grid (workgroups) used. */
+int32_t rpgpu_device_info(const rpgpu_ctx* ctx, int32_t* cu_count, int32_t* grid);
+
+/* ---- pinned host arenas ------------------------------------------------ */
+void* rpgpu_arena_alloc(rpgpu_ctx* ctx, size_t bytes);
+void rpgpu_arena_free(rpgpu_ctx* ctx, void* p);
+
+/* ---- batch validation (produce path / storage path) ---------------------
+ * Replaces, per batch:
+ *   kafka::kafka_batch_adapter::adapt        kafka/protocol/kafka_batch_adapter.cc:136-198
+ *   model::record_batch::for_each_record     model/record.h:668-691
+ *   model::crc_record_batch                  model/record_utils.cc:82-91
+ *   model::internal_header_only_crc          model/record_utils.cc:34-55
+ * and for RPGPU_FMT_RP_DISK batches the per-batch checks of
+ *   storage::continuous_batch_parser          storage/parser.cc:155-216
+ *   storage log_replayer checksumming_consumer storage/log_replayer.cc:26-92
+ *
+ * Host-memory submission: copies descriptors + data to the device, runs the
+ * kernels and copies results back, asynchronously on the context's stream.
+ * `index_cap` is the capacity of out_index in entries; entries are laid out
+ * per batch in descriptor order (index_first of result i).
+ */
+int32_t rpgpu_submit(rpgpu_ctx* ctx, const rpgpu_batch_desc* descs, uint32_t n,
+                     const void* data, size_t data_len,
+                     rpgpu_batch_result* out_results,
+                     rpgpu_record_index* out_index, uint64_t index_cap,
+                     uint64_t* out_index_used, rpgpu_ticket* ticket);
+/* 0 = done, 1 = still running, <0 = error. Never blocks. */
+int32_t rpgpu_poll(rpgpu_ctx* ctx, rpgpu_ticket ticket);
+/* Blocks until the ticket completes. */
+int32_t rpgpu_wait(rpgpu_ctx* ctx, rpgpu_ticket ticket);
+
+/* Device-resident entry point: every pointer is device memory, the work is
+ * enqueued on `hip_stream` (a hipStream_t; NULL = the context stream) and the
+ * call returns without synchronising.  `d_scratch` must hold
+ * rpgpu_validate_scratch_bytes(n) bytes.  *d_index_used receives the total
+ * number of index entries reserved. */
+size_t rpgpu_validate_scratch_bytes(uint32_t n);
+int32_t rpgpu_validate_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_descs,
+                              uint32_t n, const uint8_t* d_data,
+                              rpgpu_batch_result* d_results,
+                              rpgpu_record_index* d_index, uint64_t index_cap,
+                              uint64_t* d_index_used, void* d_scratch,
+                              void* hip_stream);
+
+/* The two halves of rpgpu_validate_device, for callers that reuse a plan or
+ * time the validation kernel on its own:
+ *   plan: per-batch index capacity + exclusive scan into d_scratch, total
+ *         into *d_index_used;
+ *   run:  the fused validate / parse / index kernel (needs the plan). */
+int32_t rpgpu_plan_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_descs, uint32_t n,
+                          const uint8_t* d_data, uint64_t* d_index_used, void* d_scratch,
+                          void* hip_stream);
+int32_t rpgpu_run_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_descs, uint32_t n,
+                         const uint8_t* d_data, rpgpu_batch_result* d_results,
+                         rpgpu_record_index* d_index, uint64_t index_cap,
+                         const void* d_scratch, void* hip_stream);
+
+/* ---- generic CRC32C over many byte ranges (device) ----------------------
+ * crc_out[i] = crc32c::Extend(seed[i] (or 0), data + off[i], len[i]) —
+ * the semantics of crc::crc32c::extend (hashing/crc32c.h:21-43). */
+int32_t rpgpu_crc32c_ranges_device(rpgpu_ctx* ctx, const uint8_t* d_data,
+                                   const uint64_t* d_off, const uint32_t* d_len,
+                                   const uint32_t* d_seed, uint32_t n,
+                                   uint32_t* d_crc_out, void* hip_stream);
+
+/* ---- synchronous scalar mirrors (run on the GPU, host pointers) ---------
+ *   crc::crc32c::extend                 hashing/crc32c.h:21-43
+ *   model::internal_header_only_crc     model/record_utils.cc:34-55
+ *   model::crc_record_batch             model/record_utils.cc:82-87
+ */
+uint32_t rpgpu_crc32c_extend(rpgpu_ctx* ctx, uint32_t crc, const void* p, size_t n);
+uint32_t rpgpu_internal_header_only_crc(rpgpu_ctx* ctx, const rpgpu_rp_header* h);
+int32_t rpgpu_crc_record_batch(rpgpu_ctx* ctx, const rpgpu_rp_header* h,
+                               const void* body, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RPGPU_H */

@@ -1,0 +1,148 @@
+"""ctypes wrapper of oracle/_build/librporacle.so (TEST INFRASTRUCTURE ONLY)."""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "_build" / "librporacle.so"
+
+# layouts identical to include/rpgpu.h (restated, not imported from the product)
+DESC_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u4"), ("partition", "<u4"),
+                       ("format", "u1"), ("ops", "u1"), ("flags", "<u2"), ("reserved", "<u4")])
+RESULT_DTYPE = np.dtype([("verdict", "<i4"), ("crc", "<u4"), ("crc_expected", "<u4"),
+                         ("header_crc", "<u4"), ("size_bytes", "<i4"), ("record_count", "<i4"),
+                         ("base_offset", "<i8"), ("last_offset_delta", "<i4"), ("attrs", "<i2"),
+                         ("codec", "u1"), ("type", "u1"), ("first_timestamp", "<i8"),
+                         ("max_timestamp", "<i8"), ("index_first", "<u4"), ("index_count", "<u4")])
+INDEX_DTYPE = np.dtype([("offset", "<i8"), ("timestamp", "<i8"), ("key_off", "<u4"),
+                        ("key_len", "<i4"), ("val_off", "<u4"), ("val_len", "<i4")])
+RP_HEADER_DTYPE = np.dtype([("header_crc", "<u4"), ("size_bytes", "<i4"), ("base_offset", "<i8"),
+                            ("type", "i1"), ("crc", "<i4"), ("attrs", "<i2"),
+                            ("last_offset_delta", "<i4"), ("first_timestamp", "<i8"),
+                            ("max_timestamp", "<i8"), ("producer_id", "<i8"),
+                            ("producer_epoch", "<i2"), ("base_sequence", "<i4"),
+                            ("record_count", "<i4")])
+
+_L = None
+
+
+def build(force: bool = False) -> Path:
+    srcs = [HERE / f for f in ("crc32c.c", "batch.c", "codec.c", "rporacle.h", "Makefile")]
+    if force or not LIB_PATH.exists() or any(s.stat().st_mtime > LIB_PATH.stat().st_mtime for s in srcs):
+        r = subprocess.run(["make", "-C", str(HERE), "-s"], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"oracle build failed:\n{r.stdout}\n{r.stderr}")
+    return LIB_PATH
+
+
+def lib() -> C.CDLL:
+    global _L
+    if _L is None:
+        build()
+        L = C.CDLL(str(LIB_PATH))
+        vp, sz, u32, u64, i32 = C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint64, C.c_int32
+        L.orc_crc32c_extend_table.restype = u32
+        L.orc_crc32c_extend_table.argtypes = [u32, vp, sz]
+        L.orc_crc32c_extend_sse42.restype = u32
+        L.orc_crc32c_extend_sse42.argtypes = [u32, vp, sz]
+        L.orc_set_fast_crc.argtypes = [C.c_int]
+        L.orc_read_varlong.restype = C.c_int64
+        L.orc_read_varlong.argtypes = [vp, sz, C.POINTER(sz), C.POINTER(u32)]
+        L.orc_write_varlong.restype = sz
+        L.orc_write_varlong.argtypes = [C.c_int64, vp]
+        L.orc_internal_header_only_crc.restype = u32
+        L.orc_internal_header_only_crc.argtypes = [vp]
+        L.orc_crc_record_batch.restype = i32
+        L.orc_crc_record_batch.argtypes = [vp, vp, sz]
+        L.orc_index_cap.restype = u32
+        L.orc_index_cap.argtypes = [vp, vp]
+        L.orc_index_total.restype = u64
+        L.orc_index_total.argtypes = [vp, u32, vp]
+        L.orc_validate_arena.restype = u64
+        L.orc_validate_arena.argtypes = [vp, u32, vp, vp, vp, u64, C.c_int]
+        L.orc_uncompress.restype = i32
+        L.orc_uncompress.argtypes = [C.c_int, vp, sz, vp, sz, C.POINTER(sz)]
+        L.orc_compress.restype = i32
+        L.orc_compress.argtypes = [C.c_int, vp, sz, vp, sz, C.POINTER(sz)]
+        L.orc_compress_bound.restype = sz
+        L.orc_compress_bound.argtypes = [C.c_int, sz]
+        _L = L
+    return _L
+
+
+def _buf(b) -> np.ndarray:
+    if isinstance(b, np.ndarray):
+        return np.ascontiguousarray(b, dtype=np.uint8)
+    return np.frombuffer(bytes(b), dtype=np.uint8)
+
+
+def crc32c(data, crc: int = 0, fast: bool = False) -> int:
+    a = _buf(data)
+    f = lib().orc_crc32c_extend_sse42 if fast else lib().orc_crc32c_extend_table
+    return int(f(crc & 0xFFFFFFFF, a.ctypes.data if a.size else None, a.size))
+
+
+def read_varlong(data, pos: int = 0) -> tuple[int, int]:
+    a = _buf(data)
+    p = C.c_size_t(pos)
+    nb = C.c_uint32()
+    v = lib().orc_read_varlong(a.ctypes.data if a.size else None, a.size, C.byref(p), C.byref(nb))
+    return int(v), int(nb.value)
+
+
+def write_varlong(v: int) -> bytes:
+    out = (C.c_uint8 * 10)()
+    n = lib().orc_write_varlong(v, out)
+    return bytes(out[:n])
+
+
+def internal_header_only_crc(hdr: np.ndarray) -> int:
+    h = np.ascontiguousarray(hdr, dtype=RP_HEADER_DTYPE).reshape(1)
+    return int(lib().orc_internal_header_only_crc(h.ctypes.data))
+
+
+def crc_record_batch(hdr: np.ndarray, body) -> int:
+    h = np.ascontiguousarray(hdr, dtype=RP_HEADER_DTYPE).reshape(1)
+    b = _buf(body)
+    return int(lib().orc_crc_record_batch(h.ctypes.data, b.ctypes.data if b.size else None, b.size))
+
+
+def validate_arena(data: np.ndarray, descs: np.ndarray, nthreads: int = 1, fast_crc: bool = False):
+    """Reference outcome for every batch of an arena: (results, index, used)."""
+    L = lib()
+    L.orc_set_fast_crc(1 if fast_crc else 0)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    descs = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+    n = len(descs)
+    cap = int(L.orc_index_total(descs.ctypes.data, n, data.ctypes.data))
+    res = np.zeros(n, dtype=RESULT_DTYPE)
+    idx = np.zeros(max(cap, 1), dtype=INDEX_DTYPE)
+    used = L.orc_validate_arena(descs.ctypes.data, n, data.ctypes.data, res.ctypes.data,
+                                idx.ctypes.data, cap, nthreads)
+    return res, idx[:used], int(used)
+
+
+def uncompress(codec: int, data, cap: int | None = None) -> tuple[int, bytes]:
+    a = _buf(data)
+    cap = cap if cap is not None else max(1 << 16, a.size * 300)
+    out = np.zeros(cap, dtype=np.uint8)
+    n = C.c_size_t()
+    v = lib().orc_uncompress(codec, a.ctypes.data if a.size else None, a.size, out.ctypes.data, cap,
+                             C.byref(n))
+    return int(v), out[: min(n.value, cap)].tobytes()
+
+
+def compress(codec: int, data) -> bytes:
+    a = _buf(data)
+    cap = int(lib().orc_compress_bound(codec, a.size))
+    out = np.zeros(cap, dtype=np.uint8)
+    n = C.c_size_t()
+    v = lib().orc_compress(codec, a.ctypes.data if a.size else None, a.size, out.ctypes.data, cap,
+                           C.byref(n))
+    if v != 0:
+        raise RuntimeError(f"compress({codec}) -> {v}")
+    return out[: n.value].tobytes()

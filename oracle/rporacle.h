@@ -1,0 +1,85 @@
+/*
+ * rporacle.h — CPU restatement of the reference's record-batch hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in redpanda_amd/ links, imports or
+ * executes this code; it is the checker for the parity tests (tests/), for
+ * __graft_entry__.smoke() and the cpu_baseline leg of bench.py.
+ *
+ * Each function cites the reference file:line it restates (paths relative to
+ * /root/reference/src/v).  Structure layouts and verdict codes are the ones
+ * declared by the product's public C ABI (include/rpgpu.h) so results can be
+ * compared byte for byte.
+ */
+#ifndef RPORACLE_H
+#define RPORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../include/rpgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* crc32c::Extend semantics (google/crc32c 1.1.2, called from
+ * hashing/crc32c.h:28-30): Extend(0, p, n) is the standard CRC32C. */
+uint32_t orc_crc32c_extend_table(uint32_t crc, const uint8_t* p, size_t n);
+uint32_t orc_crc32c_extend_sse42(uint32_t crc, const uint8_t* p, size_t n);
+int orc_have_sse42(void);
+/* select the body CRC used by the batch functions (0 = table, 1 = SSE4.2) */
+void orc_set_fast_crc(int fast);
+
+/* utils/vint.h:35-64,154-161 via bytes/iobuf_parser.h:48-52 */
+int64_t orc_read_varlong(const uint8_t* p, size_t n, size_t* pos, uint32_t* nbytes);
+/* utils/vint.h:133-149 */
+size_t orc_write_varlong(int64_t v, uint8_t* out);
+
+/* model/record_utils.cc:34-55 */
+uint32_t orc_internal_header_only_crc(const rpgpu_rp_header* h);
+/* model/record_utils.cc:68-87 */
+int32_t orc_crc_record_batch(const rpgpu_rp_header* h, const uint8_t* body, size_t n);
+
+/* Index capacity reserved for one batch (same rule as the engine). */
+uint32_t orc_index_cap(const rpgpu_batch_desc* d, const uint8_t* data);
+uint64_t orc_index_total(const rpgpu_batch_desc* descs, uint32_t n, const uint8_t* data);
+
+/* One batch of the produce path: kafka_batch_adapter::adapt
+ * (kafka/protocol/kafka_batch_adapter.cc:136-198) followed by the
+ * for_each_record walk (model/record.h:668-691).  Returns index entries
+ * written (<= cap).  `batch_off` is the arena offset of p (index spans are
+ * batch-relative, so it is unused except for documentation). */
+uint32_t orc_kafka_adapt(const uint8_t* p, uint32_t len, uint8_t ops,
+                         rpgpu_batch_result* res, rpgpu_record_index* idx, uint32_t cap);
+
+/* One on-disk batch: storage/parser.cc:155-216 header checks followed by
+ * the checksumming consumer (storage/log_replayer.cc:47-80) and an optional
+ * record walk. */
+uint32_t orc_disk_batch(const uint8_t* p, uint32_t len, uint8_t ops,
+                        rpgpu_batch_result* res, rpgpu_record_index* idx, uint32_t cap);
+
+/* Whole arena, descriptor order, index laid out by exclusive scan of
+ * orc_index_cap.  nthreads > 1 runs partitions round-robin over pthreads
+ * (Seastar shard-per-core model).  Returns the total index entries reserved. */
+uint64_t orc_validate_arena(const rpgpu_batch_desc* descs, uint32_t n,
+                            const uint8_t* data, rpgpu_batch_result* res,
+                            rpgpu_record_index* idx, uint64_t index_cap,
+                            int nthreads);
+
+/* ---- codecs (compression/compression.cc:35-55) ---------------------------
+ * Returns an rpgpu_verdict; *out_len receives the produced bytes (which may
+ * be a partial output when the reference reports success on a truncated
+ * frame).  If the output would exceed `cap`, returns RPGPU_V_DECOMP_OVERFLOW
+ * with *out_len = required size when known. */
+int32_t orc_uncompress(int codec, const uint8_t* in, size_t n, uint8_t* out,
+                       size_t cap, size_t* out_len);
+/* compress with the reference's settings (lz4_frame_compressor.cc:68-158,
+ * stream_zstd.cc:89-151, snappy_java_compressor.cc:58-75). */
+int32_t orc_compress(int codec, const uint8_t* in, size_t n, uint8_t* out,
+                     size_t cap, size_t* out_len);
+size_t orc_compress_bound(int codec, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

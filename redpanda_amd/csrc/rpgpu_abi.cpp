@@ -1,0 +1,394 @@
+// rpgpu_abi.cpp — the extern "C" boundary (include/rpgpu.h).
+//
+// Host side of the engine: device contexts, pinned arenas, asynchronous
+// submissions with tickets, and the synchronous scalar mirrors.  Every
+// computation runs on the GPU; the host only moves bytes and sequences
+// launches.  Nothing here throws across the ABI.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "rpgpu.h"
+#include "rpgpu_internal.h"
+
+namespace rpgpu {
+hipError_t launch_validate(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
+                           rpgpu_batch_result* d_res, rpgpu_record_index* d_index, uint64_t index_cap,
+                           uint64_t* d_index_used, void* d_scratch, const uint32_t* d_tables, int grid,
+                           hipStream_t s);
+hipError_t launch_crc_ranges(const uint8_t* d_data, const uint64_t* d_off, const uint32_t* d_len,
+                             const uint32_t* d_seed, uint32_t n, uint32_t* d_out, const uint32_t* d_tables,
+                             int grid, hipStream_t s);
+size_t validate_scratch_bytes(uint32_t n);
+hipError_t launch_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
+                       uint64_t* d_index_used, void* d_scratch, hipStream_t s);
+hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
+                      rpgpu_batch_result* d_res, rpgpu_record_index* d_index, uint64_t index_cap,
+                      const void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s);
+}  // namespace rpgpu
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t size = 0;
+    hipError_t reserve(size_t want) {
+        if (want <= size) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        size = 0;
+        size_t sz = want < 4096 ? 4096 : want + want / 4;
+        hipError_t e = hipMalloc(&p, sz);
+        if (e == hipSuccess) size = sz;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        size = 0;
+    }
+};
+
+struct Ticket {
+    hipEvent_t ev1 = nullptr;  // kernels + results copy-back
+    hipEvent_t ev2 = nullptr;  // index copy-back
+    int phase = 0;             // 0 free, 1 running, 2 index copy, 3 done
+    int32_t status = RPGPU_OK;
+    rpgpu_record_index* out_index = nullptr;
+    uint64_t index_cap = 0;
+    uint64_t* out_used = nullptr;
+    uint64_t* h_used = nullptr;  // pinned
+    size_t d_index_off = 0;
+};
+
+}  // namespace
+
+struct rpgpu_ctx {
+    int device = 0;
+    int cu_count = 0;
+    int grid = 0;
+    hipStream_t stream = nullptr;
+    uint32_t* d_tables = nullptr;
+    DevBuf work;     // submissions: descs | data | results | index | scratch | used
+    DevBuf small;    // scalar mirrors
+    std::vector<Ticket> tickets;
+    uint64_t next_ticket = 1;
+    bool busy = false;  // one in-flight submission per context (shard-owned)
+    std::string err;
+};
+
+namespace {
+int32_t fail(rpgpu_ctx* c, hipError_t e, const char* what) {
+    if (c) {
+        c->err = std::string(what) + ": " + hipGetErrorString(e);
+    }
+    return e == hipErrorOutOfMemory ? RPGPU_ENOMEM : RPGPU_EDEVICE;
+}
+size_t align_up(size_t v, size_t a) { return (v + a - 1) & ~(a - 1); }
+}  // namespace
+
+extern "C" {
+
+int32_t rpgpu_abi_version(void) { return RPGPU_ABI_VERSION; }
+
+rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
+    (void)opts;
+    rpgpu_ctx* c = new (std::nothrow) rpgpu_ctx();
+    if (!c) return nullptr;
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess) {
+        delete c;
+        return nullptr;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        delete c;
+        return nullptr;
+    }
+    c->cu_count = prop.multiProcessorCount;
+    // 3 workgroups of 8 waves per CU: the 45 KiB of LDS tables admit 3.
+    c->grid = c->cu_count * 3;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return nullptr;
+    }
+    std::vector<uint32_t> t(rpgpu::kTableWords);
+    rpgpu::build_tables(t.data());
+    if (hipMalloc(&c->d_tables, sizeof(uint32_t) * t.size()) != hipSuccess ||
+        hipMemcpy(c->d_tables, t.data(), sizeof(uint32_t) * t.size(), hipMemcpyHostToDevice) !=
+            hipSuccess) {
+        rpgpu_close(c);
+        return nullptr;
+    }
+    return c;
+}
+
+void rpgpu_close(rpgpu_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& t : c->tickets) {
+        if (t.ev1) (void)hipEventDestroy(t.ev1);
+        if (t.ev2) (void)hipEventDestroy(t.ev2);
+        if (t.h_used) (void)hipHostFree(t.h_used);
+    }
+    c->work.release();
+    c->small.release();
+    if (c->d_tables) (void)hipFree(c->d_tables);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* rpgpu_last_error(const rpgpu_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int32_t rpgpu_device_info(const rpgpu_ctx* c, int32_t* cu_count, int32_t* grid) {
+    if (!c) return RPGPU_EINVAL;
+    if (cu_count) *cu_count = c->cu_count;
+    if (grid) *grid = c->grid;
+    return RPGPU_OK;
+}
+
+void* rpgpu_arena_alloc(rpgpu_ctx* c, size_t bytes) {
+    void* p = nullptr;
+    if (!c) return nullptr;
+    (void)hipSetDevice(c->device);
+    if (hipHostMalloc(&p, bytes + RPGPU_ARENA_TAIL_PAD, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void rpgpu_arena_free(rpgpu_ctx* c, void* p) {
+    (void)c;
+    if (p) (void)hipHostFree(p);
+}
+
+size_t rpgpu_validate_scratch_bytes(uint32_t n) { return rpgpu::validate_scratch_bytes(n); }
+
+int32_t rpgpu_validate_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, uint32_t n,
+                              const uint8_t* d_data, rpgpu_batch_result* d_results,
+                              rpgpu_record_index* d_index, uint64_t index_cap, uint64_t* d_index_used,
+                              void* d_scratch, void* hip_stream) {
+    if (!c || (n && (!d_descs || !d_data || !d_results || !d_scratch))) return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_validate(d_descs, n, d_data, d_results, d_index, d_index ? index_cap : 0,
+                                          d_index_used, d_scratch, c->d_tables, c->grid, s);
+    if (e != hipSuccess) return fail(c, e, "validate launch");
+    return RPGPU_OK;
+}
+
+int32_t rpgpu_plan_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, uint32_t n,
+                          const uint8_t* d_data, uint64_t* d_index_used, void* d_scratch,
+                          void* hip_stream) {
+    if (!c || (n && (!d_descs || !d_data || !d_scratch))) return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_plan(d_descs, n, d_data, d_index_used, d_scratch, s);
+    if (e != hipSuccess) return fail(c, e, "plan launch");
+    return RPGPU_OK;
+}
+
+int32_t rpgpu_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
+                         rpgpu_batch_result* d_results, rpgpu_record_index* d_index, uint64_t index_cap,
+                         const void* d_scratch, void* hip_stream) {
+    if (!c || (n && (!d_descs || !d_data || !d_results || !d_scratch))) return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_run(d_descs, n, d_data, d_results, d_index, d_index ? index_cap : 0,
+                                     d_scratch, c->d_tables, c->grid, s);
+    if (e != hipSuccess) return fail(c, e, "run launch");
+    return RPGPU_OK;
+}
+
+int32_t rpgpu_crc32c_ranges_device(rpgpu_ctx* c, const uint8_t* d_data, const uint64_t* d_off,
+                                   const uint32_t* d_len, const uint32_t* d_seed, uint32_t n,
+                                   uint32_t* d_crc_out, void* hip_stream) {
+    if (!c || (n && (!d_data || !d_off || !d_len || !d_crc_out))) return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_crc_ranges(d_data, d_off, d_len, d_seed, n, d_crc_out, c->d_tables,
+                                            c->grid, s);
+    if (e != hipSuccess) return fail(c, e, "crc launch");
+    return RPGPU_OK;
+}
+
+int32_t rpgpu_submit(rpgpu_ctx* c, const rpgpu_batch_desc* descs, uint32_t n, const void* data,
+                     size_t data_len, rpgpu_batch_result* out_results, rpgpu_record_index* out_index,
+                     uint64_t index_cap, uint64_t* out_index_used, rpgpu_ticket* ticket) {
+    if (!c || !ticket || (n && (!descs || !data || !out_results))) return RPGPU_EINVAL;
+    if (c->busy) {
+        c->err = "a submission is still in flight on this context";
+        return RPGPU_EINVAL;
+    }
+    (void)hipSetDevice(c->device);
+    if (!out_index) index_cap = 0;
+    const size_t o_desc = 0;
+    const size_t o_data = align_up(o_desc + sizeof(rpgpu_batch_desc) * (size_t)n, 256);
+    const size_t o_res = align_up(o_data + data_len + RPGPU_ARENA_TAIL_PAD, 256);
+    const size_t o_idx = align_up(o_res + sizeof(rpgpu_batch_result) * (size_t)n, 256);
+    const size_t o_scr = align_up(o_idx + sizeof(rpgpu_record_index) * (size_t)index_cap, 256);
+    const size_t o_used = align_up(o_scr + rpgpu::validate_scratch_bytes(n), 256);
+    const size_t total = o_used + 64;
+    hipError_t e = c->work.reserve(total);
+    if (e != hipSuccess) return fail(c, e, "device buffer");
+    uint8_t* base = static_cast<uint8_t*>(c->work.p);
+    hipStream_t s = c->stream;
+    if ((e = hipMemcpyAsync(base + o_desc, descs, sizeof(rpgpu_batch_desc) * n, hipMemcpyHostToDevice, s)) !=
+            hipSuccess ||
+        (e = hipMemcpyAsync(base + o_data, data, data_len, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemsetAsync(base + o_data + data_len, 0, RPGPU_ARENA_TAIL_PAD, s)) != hipSuccess)
+        return fail(c, e, "upload");
+    e = rpgpu::launch_validate(reinterpret_cast<rpgpu_batch_desc*>(base + o_desc), n, base + o_data,
+                               reinterpret_cast<rpgpu_batch_result*>(base + o_res),
+                               reinterpret_cast<rpgpu_record_index*>(base + o_idx), index_cap,
+                               reinterpret_cast<uint64_t*>(base + o_used), base + o_scr, c->d_tables,
+                               c->grid, s);
+    if (e != hipSuccess) return fail(c, e, "validate launch");
+    Ticket* t = nullptr;
+    for (auto& x : c->tickets)
+        if (x.phase == 0) t = &x;
+    if (!t) {
+        c->tickets.emplace_back();
+        t = &c->tickets.back();
+    }
+    if (!t->ev1 && hipEventCreateWithFlags(&t->ev1, hipEventDisableTiming) != hipSuccess)
+        return fail(c, hipErrorUnknown, "event");
+    if (!t->ev2 && hipEventCreateWithFlags(&t->ev2, hipEventDisableTiming) != hipSuccess)
+        return fail(c, hipErrorUnknown, "event");
+    if (!t->h_used && hipHostMalloc(reinterpret_cast<void**>(&t->h_used), 64, hipHostMallocDefault) != hipSuccess)
+        return fail(c, hipErrorOutOfMemory, "pinned");
+    if ((e = hipMemcpyAsync(out_results, base + o_res, sizeof(rpgpu_batch_result) * n, hipMemcpyDeviceToHost,
+                            s)) != hipSuccess ||
+        (e = hipMemcpyAsync(t->h_used, base + o_used, sizeof(uint64_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipEventRecord(t->ev1, s)) != hipSuccess)
+        return fail(c, e, "download");
+    t->phase = 1;
+    t->status = RPGPU_OK;
+    t->out_index = out_index;
+    t->index_cap = index_cap;
+    t->out_used = out_index_used;
+    t->d_index_off = o_idx;
+    c->busy = true;
+    *ticket = (uint64_t)(t - c->tickets.data()) + 1;
+    return RPGPU_OK;
+}
+
+static int32_t advance(rpgpu_ctx* c, Ticket& t, bool block) {
+    if (t.phase == 1) {
+        hipError_t q = block ? hipEventSynchronize(t.ev1) : hipEventQuery(t.ev1);
+        if (q == hipErrorNotReady) return RPGPU_PENDING;
+        if (q != hipSuccess) {
+            t.phase = 3;
+            t.status = fail(c, q, "submission");
+        } else {
+            const uint64_t used = *t.h_used;
+            if (t.out_used) *t.out_used = used;
+            const uint64_t ncopy = used < t.index_cap ? used : t.index_cap;
+            if (used > t.index_cap) t.status = RPGPU_ECAPACITY;
+            if (ncopy && t.out_index) {
+                hipError_t e = hipMemcpyAsync(t.out_index, static_cast<uint8_t*>(c->work.p) + t.d_index_off,
+                                              sizeof(rpgpu_record_index) * ncopy, hipMemcpyDeviceToHost,
+                                              c->stream);
+                if (e == hipSuccess) e = hipEventRecord(t.ev2, c->stream);
+                if (e != hipSuccess) {
+                    t.phase = 3;
+                    t.status = fail(c, e, "index download");
+                } else {
+                    t.phase = 2;
+                }
+            } else {
+                t.phase = 3;
+            }
+        }
+    }
+    if (t.phase == 2) {
+        hipError_t q = block ? hipEventSynchronize(t.ev2) : hipEventQuery(t.ev2);
+        if (q == hipErrorNotReady) return RPGPU_PENDING;
+        if (q != hipSuccess) t.status = fail(c, q, "index download");
+        t.phase = 3;
+    }
+    if (t.phase == 3) {
+        t.phase = 0;
+        c->busy = false;
+        return t.status;
+    }
+    return RPGPU_EINVAL;
+}
+
+int32_t rpgpu_poll(rpgpu_ctx* c, rpgpu_ticket ticket) {
+    if (!c || ticket == 0 || ticket > c->tickets.size()) return RPGPU_EINVAL;
+    (void)hipSetDevice(c->device);
+    return advance(c, c->tickets[ticket - 1], false);
+}
+
+int32_t rpgpu_wait(rpgpu_ctx* c, rpgpu_ticket ticket) {
+    if (!c || ticket == 0 || ticket > c->tickets.size()) return RPGPU_EINVAL;
+    (void)hipSetDevice(c->device);
+    int32_t r;
+    while ((r = advance(c, c->tickets[ticket - 1], true)) == RPGPU_PENDING) {
+    }
+    return r;
+}
+
+// ---- synchronous scalar mirrors ------------------------------------------
+static int32_t crc_one(rpgpu_ctx* c, uint32_t seed, const void* p, size_t n, uint32_t* out) {
+    (void)hipSetDevice(c->device);
+    const size_t o_data = 0;
+    const size_t o_meta = align_up(n + 16, 256);
+    hipError_t e = c->small.reserve(o_meta + 64);
+    if (e != hipSuccess) return fail(c, e, "device buffer");
+    uint8_t* base = static_cast<uint8_t*>(c->small.p);
+    struct {
+        uint64_t off;
+        uint32_t len, seed, out, pad;
+    } meta = {0, (uint32_t)n, seed, 0, 0};
+    if (n && (e = hipMemcpyAsync(base + o_data, p, n, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+        return fail(c, e, "upload");
+    if ((e = hipMemcpyAsync(base + o_meta, &meta, sizeof(meta), hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+        return fail(c, e, "upload");
+    e = rpgpu::launch_crc_ranges(base, reinterpret_cast<uint64_t*>(base + o_meta),
+                                 reinterpret_cast<uint32_t*>(base + o_meta + 8),
+                                 reinterpret_cast<uint32_t*>(base + o_meta + 12), 1,
+                                 reinterpret_cast<uint32_t*>(base + o_meta + 16), c->d_tables, 1, c->stream);
+    if (e != hipSuccess) return fail(c, e, "crc launch");
+    if ((e = hipMemcpyAsync(out, base + o_meta + 16, 4, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        return fail(c, e, "download");
+    return RPGPU_OK;
+}
+
+uint32_t rpgpu_crc32c_extend(rpgpu_ctx* c, uint32_t crc, const void* p, size_t n) {
+    uint32_t out = 0;
+    if (!c || (n && !p) || n > 0xffffffffu) return 0;
+    if (crc_one(c, crc, p, n, &out) != RPGPU_OK) return 0;
+    return out;
+}
+
+uint32_t rpgpu_internal_header_only_crc(rpgpu_ctx* c, const rpgpu_rp_header* h) {
+    // model/record_utils.cc:34-55: the 57 little-endian bytes after header_crc
+    // are exactly the packed image's bytes [4, 61).
+    if (!h) return 0;
+    return rpgpu_crc32c_extend(c, 0, reinterpret_cast<const uint8_t*>(h) + 4, RPGPU_HEADER_SIZE - 4);
+}
+
+int32_t rpgpu_crc_record_batch(rpgpu_ctx* c, const rpgpu_rp_header* h, const void* body, size_t n) {
+    // model/record_utils.cc:68-87: big-endian attrs..record_count, then body.
+    if (!h) return 0;
+    std::vector<uint8_t> buf(40 + n);
+    uint8_t* q = buf.data();
+    auto be = [&](uint64_t v, int nb) {
+        for (int i = 0; i < nb; i++) *q++ = (uint8_t)(v >> (8 * (nb - 1 - i)));
+    };
+    be((uint16_t)h->attrs, 2);
+    be((uint32_t)h->last_offset_delta, 4);
+    be((uint64_t)h->first_timestamp, 8);
+    be((uint64_t)h->max_timestamp, 8);
+    be((uint64_t)h->producer_id, 8);
+    be((uint16_t)h->producer_epoch, 2);
+    be((uint32_t)h->base_sequence, 4);
+    be((uint32_t)h->record_count, 4);
+    if (n) memcpy(q, body, n);
+    return (int32_t)rpgpu_crc32c_extend(c, 0, buf.data(), buf.size());
+}
+
+}  // extern "C"

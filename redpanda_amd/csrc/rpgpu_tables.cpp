@@ -1,0 +1,67 @@
+// rpgpu_tables.cpp — CRC32C lookup tables for the strided-row kernels.
+//
+// All tables are images of GF(2)-linear maps on the 32-bit reflected CRC
+// state (Castagnoli polynomial 0x82F63B78, the polynomial google/crc32c
+// implements for crc::crc32c, hashing/crc32c.h:21-43):
+//   S_k   = advance the state over k zero bytes (k may be negative: the map is
+//           invertible because the polynomial has a non-zero constant term);
+//   V[j]  = S_{j+1008} o T0 for j = 0..15  (slice-by-16 with the 1008-byte
+//           gap between one lane's consecutive blocks folded in);
+//   W[s]  = S_{-16*2^s} split into 4 byte tables (butterfly combine);
+//   H     = S_{-960} (header-CRC window correction);
+//   T0    = the plain byte table.
+#include <stdint.h>
+#include <string.h>
+
+#include "rpgpu_internal.h"
+
+namespace rpgpu {
+namespace {
+constexpr uint32_t kPoly = 0x82F63B78u;
+
+uint32_t bit_fwd(uint32_t c) { return (c & 1) ? (c >> 1) ^ kPoly : (c >> 1); }
+uint32_t bit_back(uint32_t c) { return (c & 0x80000000u) ? ((c ^ kPoly) << 1) | 1u : (c << 1); }
+
+// images of the 32 basis vectors under S_k (k in bytes, signed)
+void shift_basis(int64_t k, uint32_t basis[32]) {
+    for (int i = 0; i < 32; i++) {
+        uint32_t c = 1u << i;
+        if (k >= 0)
+            for (int64_t b = 0; b < 8 * k; b++) c = bit_fwd(c);
+        else
+            for (int64_t b = 0; b < -8 * k; b++) c = bit_back(c);
+        basis[i] = c;
+    }
+}
+uint32_t apply_basis(const uint32_t basis[32], uint32_t v) {
+    uint32_t r = 0;
+    for (int i = 0; i < 32; i++)
+        if (v >> i & 1) r ^= basis[i];
+    return r;
+}
+void byte_tables(int64_t k, uint32_t* out /* 4 x 256 */) {
+    uint32_t basis[32];
+    shift_basis(k, basis);
+    for (int j = 0; j < 4; j++)
+        for (uint32_t b = 0; b < 256; b++) out[j * 256 + b] = apply_basis(basis, b << (8 * j));
+}
+}  // namespace
+
+void build_tables(uint32_t* out) {
+    memset(out, 0, sizeof(uint32_t) * kTableWords);
+    uint32_t* t0 = out + kOffT0;
+    for (uint32_t b = 0; b < 256; b++) {
+        uint32_t c = b;
+        for (int k = 0; k < 8; k++) c = bit_fwd(c);
+        t0[b] = c;
+    }
+    for (int j = 0; j < 16; j++) {
+        uint32_t basis[32];
+        shift_basis(j + 1008, basis);
+        for (uint32_t b = 0; b < 256; b++) out[kOffV + j * 256 + b] = apply_basis(basis, t0[b]);
+    }
+    for (int s = 0; s < 6; s++) byte_tables(-16ll * (1ll << s), out + kOffW + s * 1024);
+    byte_tables(-960, out + kOffH);
+}
+
+}  // namespace rpgpu

@@ -1,0 +1,168 @@
+"""Engine: a device context plus arena submission (host or device resident).
+
+Every call runs on the GPU through librpgpu.so; there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+class Engine:
+    """One rpgpu context (one per Seastar shard x GPU in the reference's terms)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = abi.lib()
+        self._ctx = self._lib.rpgpu_open(device, None)
+        if not self._ctx:
+            raise EngineError(f"rpgpu_open({device}) failed (no usable HIP device?)")
+        self.device = device
+
+    # -- lifetime ---------------------------------------------------------------
+    def close(self) -> None:
+        if self._ctx:
+            self._lib.rpgpu_close(self._ctx)
+            self._ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ctx(self):
+        return self._ctx
+
+    def last_error(self) -> str:
+        return self._lib.rpgpu_last_error(self._ctx).decode()
+
+    def device_info(self) -> tuple[int, int]:
+        cu, grid = C.c_int32(), C.c_int32()
+        self._lib.rpgpu_device_info(self._ctx, C.byref(cu), C.byref(grid))
+        return cu.value, grid.value
+
+    # -- host-memory submission (rpgpu_submit / rpgpu_wait) -----------------------
+    def submit(self, data: np.ndarray, descs: np.ndarray, index_cap: int | None = None):
+        """Validate an arena held in host memory.  Returns (results, index, used)."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        descs = np.ascontiguousarray(descs, dtype=abi.DESC_DTYPE)
+        n = len(descs)
+        if index_cap is None:
+            index_cap = int(descs["length"].astype(np.uint64).sum() // 2) + 1
+        results = np.zeros(n, dtype=abi.RESULT_DTYPE)
+        index = np.zeros(max(index_cap, 1), dtype=abi.INDEX_DTYPE)
+        used = C.c_uint64()
+        ticket = C.c_uint64()
+        rc = self._lib.rpgpu_submit(self._ctx, descs.ctypes.data, n, data.ctypes.data, data.nbytes,
+                                    results.ctypes.data, index.ctypes.data, index_cap,
+                                    C.byref(used), C.byref(ticket))
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_submit: {rc} {self.last_error()}")
+        rc = self._lib.rpgpu_wait(self._ctx, ticket.value)
+        if rc not in (abi.RPGPU_OK, abi.RPGPU_ECAPACITY):
+            raise EngineError(f"rpgpu_wait: {rc} {self.last_error()}")
+        return results, index[: min(used.value, index_cap)], used.value
+
+    # -- device-resident submission (rpgpu_validate_device) ------------------------
+    @staticmethod
+    def scratch_bytes(n: int) -> int:
+        return int(abi.lib().rpgpu_validate_scratch_bytes(n))
+
+    def validate_device(self, d_descs: int, n: int, d_data: int, d_results: int, d_index: int,
+                        index_cap: int, d_used: int, d_scratch: int, stream: int = 0) -> None:
+        rc = self._lib.rpgpu_validate_device(self._ctx, d_descs, n, d_data, d_results, d_index,
+                                             index_cap, d_used, d_scratch, stream or None)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_validate_device: {rc} {self.last_error()}")
+
+    def plan_device(self, d_descs: int, n: int, d_data: int, d_used: int, d_scratch: int,
+                    stream: int = 0) -> None:
+        rc = self._lib.rpgpu_plan_device(self._ctx, d_descs, n, d_data, d_used, d_scratch,
+                                         stream or None)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_plan_device: {rc} {self.last_error()}")
+
+    def run_device(self, d_descs: int, n: int, d_data: int, d_results: int, d_index: int,
+                   index_cap: int, d_scratch: int, stream: int = 0) -> None:
+        rc = self._lib.rpgpu_run_device(self._ctx, d_descs, n, d_data, d_results, d_index,
+                                        index_cap, d_scratch, stream or None)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_run_device: {rc} {self.last_error()}")
+
+    def crc32c_ranges_device(self, d_data: int, d_off: int, d_len: int, d_seed: int, n: int,
+                             d_out: int, stream: int = 0) -> None:
+        rc = self._lib.rpgpu_crc32c_ranges_device(self._ctx, d_data, d_off, d_len, d_seed or None,
+                                                  n, d_out, stream or None)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_crc32c_ranges_device: {rc} {self.last_error()}")
+
+    # -- synchronous scalar mirrors ---------------------------------------------------
+    def crc32c_extend(self, crc: int, data: bytes | np.ndarray) -> int:
+        buf = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        return int(self._lib.rpgpu_crc32c_extend(self._ctx, crc & 0xFFFFFFFF,
+                                                 buf.ctypes.data if buf.size else None, buf.size))
+
+    def internal_header_only_crc(self, hdr: np.ndarray) -> int:
+        h = np.ascontiguousarray(hdr, dtype=abi.RP_HEADER_DTYPE).reshape(1)
+        return int(self._lib.rpgpu_internal_header_only_crc(self._ctx, h.ctypes.data))
+
+    def crc_record_batch(self, hdr: np.ndarray, body: bytes | np.ndarray) -> int:
+        h = np.ascontiguousarray(hdr, dtype=abi.RP_HEADER_DTYPE).reshape(1)
+        b = np.ascontiguousarray(np.frombuffer(bytes(body), dtype=np.uint8))
+        return int(self._lib.rpgpu_crc_record_batch(self._ctx, h.ctypes.data,
+                                                    b.ctypes.data if b.size else None, b.size))
+
+
+# ---- workload construction (librpgen.so) -----------------------------------------
+def make_spec(**kw) -> abi.GenSpec:
+    s = abi.GenSpec()
+    defaults = dict(seed=0x5EED0002, partitions=1, records_per_batch=16, key_len=16, value_len=995,
+                    headers_per_record=0, header_key_len=0, header_value_len=0,
+                    format=abi.FMT_KAFKA_WIRE, ops=abi.OPS_PRODUCE, codec=0,
+                    payload=abi.PAYLOAD_ALNUM, codec_mix=0, body_min=0, body_max=0,
+                    corrupt_ppm=0, corrupt_mask=0, base_timestamp=1_700_000_000_000)
+    defaults.update(kw)
+    for k, v in defaults.items():
+        setattr(s, k, v)
+    return s
+
+
+def build_arena(spec: abi.GenSpec, n: int, first: int = 0, nthreads: int | None = None,
+                out: np.ndarray | None = None):
+    """Generate batches [first, first+n) into a contiguous arena.
+
+    Returns (data uint8 array incl. tail pad, descs).  `out` may be a
+    preallocated (e.g. pinned) uint8 array."""
+    g = abi.gen()
+    nthreads = nthreads or min(16, os.cpu_count() or 1)
+    used = C.c_uint64()
+    descs = np.zeros(n, dtype=abi.DESC_DTYPE)
+    rc = g.rpgen_build(C.byref(spec), first, n, None, 0, descs.ctypes.data, C.byref(used), nthreads)
+    if rc != 0:
+        raise EngineError(f"rpgen_build size pass: {rc}")
+    size = used.value + abi.ARENA_TAIL_PAD
+    if out is None:
+        out = np.empty(size, dtype=np.uint8)
+    elif out.nbytes < size:
+        raise EngineError(f"arena buffer too small: {out.nbytes} < {size}")
+    rc = g.rpgen_build(C.byref(spec), first, n, out.ctypes.data, out.nbytes, descs.ctypes.data,
+                       C.byref(used), nthreads)
+    if rc != 0:
+        raise EngineError(f"rpgen_build: {rc}")
+    return out[:size], descs
