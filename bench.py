@@ -58,6 +58,7 @@ def main() -> int:
     ap.add_argument("--batches", type=int, default=0, help="override batches per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--ops", type=int, default=0, help="override the rpgpu_op mask (diagnostics)")
     args = ap.parse_args()
 
     import torch
@@ -78,6 +79,8 @@ def main() -> int:
     P = cfg["partitions"]
     spec = engine.make_spec(seed=0x5EED0000 + (2 if args.config == "c2" else 1), partitions=P,
                             **cfg["spec"])
+    if args.ops:
+        spec.ops = args.ops
     eng = engine.Engine(local)
     nthreads = int(os.environ.get("OMP_NUM_THREADS", "16"))
     nthreads = max(1, min(nthreads, 16))
@@ -128,7 +131,9 @@ def main() -> int:
     d_res = torch.zeros(n * 64, dtype=torch.uint8, device=dev)
     d_scratch = torch.zeros(engine.Engine.scratch_bytes(n), dtype=torch.uint8, device=dev)
     d_used = torch.zeros(1, dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated stream: the engine and the timing events must share it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
 
     # plan once to size the record index

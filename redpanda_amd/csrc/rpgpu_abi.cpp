@@ -111,8 +111,8 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
         return nullptr;
     }
     c->cu_count = prop.multiProcessorCount;
-    // 3 workgroups of 8 waves per CU: the 45 KiB of LDS tables admit 3.
-    c->grid = c->cu_count * 3;
+    // one 8-wave workgroup per CU: CRC tables + 8 x 16 KiB staging fill the LDS
+    c->grid = c->cu_count;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return nullptr;

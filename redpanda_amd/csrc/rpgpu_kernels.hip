@@ -1,6 +1,8 @@
 // rpgpu_kernels.hip — CDNA4 (gfx950) kernels of the record-batch engine.
 //
-// One wavefront owns one batch at a time (grid-stride over the arena).
+// One wavefront owns one batch at a time (grid-stride over the arena); one
+// 8-wave workgroup per CU shares the CRC tables (20.5 KiB) and gives each
+// wave a 16 KiB LDS staging buffer.
 //
 // CRC32C layout ("strided rows").  The Kafka CRC covers batch bytes
 // [21, n) (kafka_batch_adapter.cc:99-134).  That region is cut into 16-byte
@@ -20,74 +22,13 @@
 // record_utils.cc:68-80), which makes the same loop serve wire batches and
 // on-disk (little-endian) batches.
 //
-// Record walk.  The wave keeps the current 8 KiB chunk of the batch in
-// registers (32 dwords per lane, the same registers the CRC consumed) and
-// walks records with wave-uniform scalar code, fetching bytes with
-// s_set_gpr_idx + v_readlane.  The walker is a resumable state machine so a
-// record may straddle chunks; it follows model/record.h:668-691 and
-// model/record_utils.cc:93-176 exactly, including the reference quirks
-// (10-byte varint limit, silent short copies, 32-bit truncated lengths).
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-
-#include "rpgpu.h"
-#include "rpgpu_internal.h"
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// Record walk (rpgpu_walk.h): the rows are also written to the wave's LDS
+// staging buffer; batches of up to 16 rows are walked after the CRC by the
+// lane-parallel fast walk, larger ones chunk by chunk by the exact walker.
+#include "rpgpu_device.h"
+#include "rpgpu_walk.h"
 
 namespace rpgpu {
-
-// ---------------------------------------------------------------- helpers
-__device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
-    u32x4 r;
-    __builtin_memcpy(&r, p, 16);  // unaligned global_load_dwordx4
-    return r;
-}
-__device__ __forceinline__ uint32_t ld4(const uint8_t* p) {
-    uint32_t r;
-    __builtin_memcpy(&r, p, 4);
-    return r;
-}
-__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
-__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
-    return __builtin_amdgcn_readlane(v, l);
-}
-__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
-__device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
-
-// 64-byte scalar byte image, dword-addressed (constant positions fold).
-struct Img64 {
-    uint32_t w[16];
-    __device__ __forceinline__ void clear() {
-#pragma unroll
-        for (int i = 0; i < 16; i++) w[i] = 0;
-    }
-    __device__ __forceinline__ uint32_t byte(int k) const { return (w[k >> 2] >> (8 * (k & 3))) & 255u; }
-    __device__ __forceinline__ void set(int k, uint32_t b) {
-        const int s = 8 * (k & 3);
-        w[k >> 2] = (w[k >> 2] & ~(255u << s)) | ((b & 255u) << s);
-    }
-    __device__ __forceinline__ void put_le(int k, uint64_t v, int nb) {
-#pragma unroll
-        for (int i = 0; i < nb; i++) set(k + i, (uint32_t)(v >> (8 * i)));
-    }
-    __device__ __forceinline__ void put_be(int k, uint64_t v, int nb) {
-#pragma unroll
-        for (int i = 0; i < nb; i++) set(k + i, (uint32_t)(v >> (8 * (nb - 1 - i))));
-    }
-    __device__ __forceinline__ uint64_t get_le(int k, int nb) const {
-        uint64_t v = 0;
-#pragma unroll
-        for (int i = nb - 1; i >= 0; i--) v = (v << 8) | byte(k + i);
-        return v;
-    }
-    __device__ __forceinline__ uint64_t get_be(int k, int nb) const {
-        uint64_t v = 0;
-#pragma unroll
-        for (int i = 0; i < nb; i++) v = (v << 8) | byte(k + i);
-        return v;
-    }
-};
 
 // Parsed record_batch_header (model/record.h:356-440), wave-uniform.
 struct Header {
@@ -102,271 +43,6 @@ struct Header {
     int32_t base_sequence, record_count;
 };
 
-// ---------------------------------------------------------- CRC primitives
-// slice-by-16 step over one block, tables V pre-shifted by 1008 bytes.
-__device__ __forceinline__ uint32_t crc_block(const uint32_t* __restrict__ sV, u32x4 x) {
-    uint32_t c;
-    c = sV[15 * 256 + (x.x & 255)] ^ sV[14 * 256 + ((x.x >> 8) & 255)] ^
-        sV[13 * 256 + ((x.x >> 16) & 255)] ^ sV[12 * 256 + (x.x >> 24)];
-    c ^= sV[11 * 256 + (x.y & 255)] ^ sV[10 * 256 + ((x.y >> 8) & 255)] ^
-         sV[9 * 256 + ((x.y >> 16) & 255)] ^ sV[8 * 256 + (x.y >> 24)];
-    c ^= sV[7 * 256 + (x.z & 255)] ^ sV[6 * 256 + ((x.z >> 8) & 255)] ^
-         sV[5 * 256 + ((x.z >> 16) & 255)] ^ sV[4 * 256 + (x.z >> 24)];
-    c ^= sV[3 * 256 + (x.w & 255)] ^ sV[2 * 256 + ((x.w >> 8) & 255)] ^
-         sV[1 * 256 + ((x.w >> 16) & 255)] ^ sV[0 * 256 + (x.w >> 24)];
-    return c;
-}
-// linear 32-bit map given as 4 byte tables
-__device__ __forceinline__ uint32_t apply4(const uint32_t* __restrict__ t, uint32_t c) {
-    return t[c & 255] ^ t[256 + ((c >> 8) & 255)] ^ t[512 + ((c >> 16) & 255)] ^ t[768 + (c >> 24)];
-}
-// fold 64 lane states: lane 0 ends with sum_l S_{-16l}(c_l)
-__device__ __forceinline__ uint32_t combine64(const uint32_t* __restrict__ sW, uint32_t c) {
-#pragma unroll
-    for (int s = 0; s < 6; s++) {
-        uint32_t t = __shfl_down(c, 1 << s, 64);
-        c ^= apply4(sW + s * 1024, t);
-    }
-    return c;
-}
-
-// Image dword at (possibly unaligned, possibly negative) batch offset o4:
-// v_img lane m holds image bytes [4m, 4m+4).
-__device__ __forceinline__ uint32_t img_dword(uint32_t v_img, int64_t o4) {
-    const int32_t k0 = (int32_t)(o4 >> 2);
-    const uint32_t sh = (uint32_t)(o4 & 3);
-    const int32_t ka = k0 < 0 ? 0 : (k0 > 15 ? 15 : k0);
-    const int32_t kb = (k0 + 1) < 0 ? 0 : ((k0 + 1) > 15 ? 15 : (k0 + 1));
-    uint32_t lo = __builtin_amdgcn_ds_bpermute(ka << 2, v_img);
-    uint32_t hi = __builtin_amdgcn_ds_bpermute(kb << 2, v_img);
-    lo = (k0 >= 0 && k0 <= 15) ? lo : 0u;
-    hi = (k0 + 1 >= 0 && k0 + 1 <= 15) ? hi : 0u;
-    return sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
-}
-
-// ------------------------------------------------------------ record walk
-enum WState : int32_t {
-    WS_LEN = 0,
-    WS_ATTR,
-    WS_TS,
-    WS_OFF,
-    WS_KLEN,
-    WS_VLEN,
-    WS_HCOUNT,
-    WS_HK,
-    WS_HV,
-    WS_DONE
-};
-
-struct Walker {
-    int64_t pos, n;  // batch-relative
-    int64_t vacc;
-    int32_t vshift;
-    int32_t state, verdict;
-    int32_t rec, rc;
-    int64_t h, hcount;
-    int64_t ts_delta, off_delta, klen, vlen;
-    int64_t key_off, val_off;
-    uint32_t cnt, cap;
-    // record-index staging: lane (cnt & 63) holds entry cnt
-    uint32_t e0, e1, e2, e3, e4, e5, e6, e7;
-};
-
-struct EmitCtx {
-    rpgpu_record_index* idx;  // already offset to this batch's first entry
-    int64_t base_offset, first_ts;
-    bool index;
-};
-
-__device__ __forceinline__ void flush_entries(Walker& w, const EmitCtx& em, uint32_t count,
-                                              uint32_t base) {
-    const uint32_t l = lane_id();
-    if (l < count) {
-        u32x4 a = {w.e0, w.e1, w.e2, w.e3};
-        u32x4 b = {w.e4, w.e5, w.e6, w.e7};
-        u32x4* dst = reinterpret_cast<u32x4*>(em.idx + base + l);
-        dst[0] = a;
-        dst[1] = b;
-    }
-}
-
-__device__ __forceinline__ void finish_record(Walker& w, const EmitCtx& em) {
-    if (em.index && w.cnt < w.cap) {
-        const uint32_t slot = w.cnt & 63u;
-        const int64_t off = (int64_t)((uint64_t)em.base_offset + (uint64_t)(int64_t)(int32_t)w.off_delta);
-        const int64_t ts = (int64_t)((uint64_t)em.first_ts + (uint64_t)w.ts_delta);
-        const bool me = lane_id() == slot;
-        w.e0 = me ? (uint32_t)off : w.e0;
-        w.e1 = me ? (uint32_t)((uint64_t)off >> 32) : w.e1;
-        w.e2 = me ? (uint32_t)ts : w.e2;
-        w.e3 = me ? (uint32_t)((uint64_t)ts >> 32) : w.e3;
-        w.e4 = me ? (uint32_t)w.key_off : w.e4;
-        w.e5 = me ? (uint32_t)(int32_t)w.klen : w.e5;
-        w.e6 = me ? (uint32_t)w.val_off : w.e6;
-        w.e7 = me ? (uint32_t)(int32_t)w.vlen : w.e7;
-        if (slot == 63u) flush_entries(w, em, 64u, w.cnt - 63u);
-    }
-    w.cnt++;
-    w.rec++;
-    if (w.rec < w.rc) {
-        w.state = WS_LEN;
-    } else {
-        w.state = WS_DONE;
-        w.verdict = (w.pos < w.n) ? RPGPU_V_REC_TRAILING : RPGPU_V_OK;
-    }
-}
-
-// iobuf_copy (bytes/iobuf.cc:136-160): int truncation, silent short copy.
-__device__ __forceinline__ bool walker_copy(Walker& w, int64_t len) {
-    const int32_t l32 = (int32_t)(uint32_t)(uint64_t)len;
-    if (l32 < 0 || (uint32_t)l32 > kCopyLimit) {
-        w.verdict = RPGPU_V_REC_UNDEFINED;
-        w.state = WS_DONE;
-        return false;
-    }
-    const int64_t room = w.n - w.pos;
-    w.pos += ((int64_t)l32 < room) ? (int64_t)l32 : room;
-    return true;
-}
-
-__device__ __forceinline__ void walker_init(Walker& w, int64_t n, int32_t rc, uint32_t cap,
-                                            bool active) {
-    w.pos = kHeaderSize;
-    w.n = n;
-    w.vacc = 0;
-    w.vshift = 0;
-    w.rec = 0;
-    w.rc = rc;
-    w.cnt = 0;
-    w.cap = cap;
-    w.h = 0;
-    w.hcount = 0;
-    w.e0 = w.e1 = w.e2 = w.e3 = w.e4 = w.e5 = w.e6 = w.e7 = 0;
-    w.ts_delta = w.off_delta = w.klen = w.vlen = w.key_off = w.val_off = 0;
-    if (!active) {
-        w.state = WS_DONE;
-        w.verdict = RPGPU_V_OK;
-    } else if (rc <= 0) {
-        w.state = WS_DONE;
-        w.verdict = (w.pos < n) ? RPGPU_V_REC_TRAILING : RPGPU_V_OK;
-    } else {
-        w.state = WS_LEN;
-        w.verdict = RPGPU_V_OK;
-    }
-}
-
-// Advance the walk through bytes available in this chunk: batch offsets
-// [cbase, hi).  cd[] holds the chunk: byte at rel = off - cbase lives in
-// dword cd[(rel >> 10) * 4 + ((rel >> 2) & 3)] of lane (rel >> 4) & 63.
-template <int NW>
-__device__ __forceinline__ void walker_run(Walker& w, const uint32_t (&cd)[NW], int64_t cbase,
-                                           int64_t hi, const EmitCtx& em) {
-    uint32_t cached_dw = 0xffffffffu, cached = 0;
-    while (w.state != WS_DONE) {
-        if (w.state == WS_ATTR) {
-            // consume_type<int8_t> (record_utils.cc:158): throws at end
-            if (w.pos >= w.n) {
-                w.verdict = RPGPU_V_REC_ATTR_EOF;
-                w.state = WS_DONE;
-                break;
-            }
-            w.pos += 1;
-            w.state = WS_TS;
-            continue;
-        }
-        if (w.state == WS_HK && w.pos >= w.n) {
-            // remaining header iterations read (0,0) and copy nothing
-            finish_record(w, em);
-            continue;
-        }
-        // varint decode (utils/vint.h:35-64, limit 63)
-        bool complete = false;
-        while (true) {
-            if (w.vshift > 63 || w.pos >= w.n) {
-                complete = true;
-                break;
-            }
-            if (w.pos >= hi) break;  // byte is in the next chunk
-            const uint32_t rel = (uint32_t)(w.pos - cbase);
-            const uint32_t dw = rel >> 2;
-            if (dw != cached_dw) {
-                const uint32_t ai = ((rel >> 10) << 2) | ((rel >> 2) & 3u);
-                const uint32_t ln = (rel >> 4) & 63u;
-                cached = rdl(cd[__builtin_amdgcn_readfirstlane(ai)], ln);
-                cached_dw = dw;
-            }
-            const uint64_t b = (cached >> ((rel & 3u) * 8u)) & 255u;
-            w.pos += 1;
-            w.vacc |= (int64_t)((b & 127u) << (uint32_t)w.vshift);
-            if (!(b & 128u)) {
-                complete = true;
-                break;
-            }
-            w.vshift += 7;
-        }
-        if (!complete) return;
-        const uint64_t u = (uint64_t)w.vacc;
-        const int64_t v = (int64_t)((u >> 1) ^ (~(u & 1) + 1));
-        w.vacc = 0;
-        w.vshift = 0;
-        switch (w.state) {
-        case WS_LEN: w.state = WS_ATTR; break;
-        case WS_TS:
-            w.ts_delta = v;
-            w.state = WS_OFF;
-            break;
-        case WS_OFF:
-            w.off_delta = v;
-            w.state = WS_KLEN;
-            break;
-        case WS_KLEN:
-            w.klen = v;
-            w.key_off = w.pos;
-            if (v > 0 && !walker_copy(w, v)) break;
-            w.state = WS_VLEN;
-            break;
-        case WS_VLEN:
-            w.vlen = v;
-            w.val_off = w.pos;
-            if (v > 0 && !walker_copy(w, v)) break;
-            w.state = WS_HCOUNT;
-            break;
-        case WS_HCOUNT:
-            if (v < 0) {  // headers.reserve(negative) -> std::length_error
-                w.verdict = RPGPU_V_REC_HCOUNT_NEG;
-                w.state = WS_DONE;
-                break;
-            }
-            if (v > kHcountLimit) {
-                w.verdict = RPGPU_V_REC_UNDEFINED;
-                w.state = WS_DONE;
-                break;
-            }
-            w.hcount = v;
-            w.h = 0;
-            if (v == 0)
-                finish_record(w, em);
-            else
-                w.state = WS_HK;
-            break;
-        case WS_HK:
-            if (v > 0 && !walker_copy(w, v)) break;
-            w.state = WS_HV;
-            break;
-        case WS_HV:
-            if (v > 0 && !walker_copy(w, v)) break;
-            w.h += 1;
-            if (w.h < w.hcount)
-                w.state = WS_HK;
-            else
-                finish_record(w, em);
-            break;
-        default: break;
-        }
-    }
-}
-
-// ------------------------------------------------------------ batch kernel
 struct Result {
     int32_t verdict;
     uint32_t crc, crc_expected, header_crc;
@@ -420,17 +96,16 @@ __device__ __forceinline__ uint32_t header_crc_vec(const uint32_t* sT, const Img
 #pragma unroll
     for (int s = 0; s < 2; s++) {
         uint32_t t = __shfl_down(c, 1 << s, 64);
-        c ^= apply4(sW + s * 1024, t);
+        c ^= apply8(sW + s * 128, t);
     }
-    c = apply4(sT + kOffH, c);
+    c = apply8(sT + kOffH, c);
     return ~rdl(c, 0);
 }
 
-template <int ROWS>
-__device__ void process_batch(const uint32_t* __restrict__ sT, const rpgpu_batch_desc& d,
-                              const uint8_t* __restrict__ data, rpgpu_batch_result* __restrict__ res,
-                              rpgpu_record_index* __restrict__ index, uint32_t index_first,
-                              uint32_t cap) {
+__device__ void process_batch(const uint32_t* __restrict__ sT, uint32_t* __restrict__ stg,
+                              const rpgpu_batch_desc& d, const uint8_t* __restrict__ data,
+                              rpgpu_batch_result* __restrict__ res, rpgpu_record_index* __restrict__ index,
+                              uint32_t index_first, uint32_t cap) {
     const uint32_t l = lane_id();
     const uint8_t* p = data + d.offset;
     const uint32_t len = d.length;
@@ -515,7 +190,7 @@ __device__ void process_batch(const uint32_t* __restrict__ sT, const rpgpu_batch
         uint32_t any = 0;
 #pragma unroll
         for (int j = 0; j < 15; j++) any |= H.w[j];
-        any |= H.w[15] & 0xffu;  // bytes 60 only (61..63 are past the header)
+        any |= H.w[15] & 0xffu;  // byte 60 only (61..63 are past the header)
         if (any == 0) {
             r.verdict = RPGPU_V_FALLOCATED_ZERO;
             write_result(res, r);
@@ -575,35 +250,34 @@ __device__ void process_batch(const uint32_t* __restrict__ sT, const rpgpu_batch
 
     const uint8_t codec = (uint8_t)(r.h.attrs & 7);
     const bool walk = !body_trunc && codec == 0 && (d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX));
-    Walker w;
-    walker_init(w, n, r.h.record_count, cap, walk);
     EmitCtx em{index + index_first, r.h.base_offset, r.h.first_ts, (d.ops & RPGPU_OP_INDEX) != 0};
 
     // ---- rows over the CRC region [21, n)
     const int64_t nblocks = (n - 21 + 15) >> 4;
     const int64_t niter = (nblocks + 63) >> 6;
     const int64_t g0 = n - (niter << 10);
+    const bool whole = niter <= kRowsPerChunk;  // batch fits the staging buffer
+    // exact walker state for batches walked chunk by chunk (large batches only)
+    Walker w;
+    if (walk && !whole) walker_init(w, n, r.h.record_count, cap, true);
     const uint32_t* sV = sT + kOffV;
     uint32_t c = 0;
-    for (int64_t cb = 0; cb < niter; cb += ROWS) {
-        uint32_t cd[ROWS * 4];
+    for (int64_t cb = 0; cb < niter; cb += kRowsPerChunk) {
+        u32x4 x[kRowsPerChunk];
 #pragma unroll
-        for (int r8 = 0; r8 < ROWS; r8++) {
-            const int64_t ro = g0 + ((cb + r8) << 10) + 16 * (int64_t)l;
-            u32x4 x = {0, 0, 0, 0};
-            if (cb + r8 < niter && ro + 16 > 21) x = ld16(p + ro);
-            cd[4 * r8 + 0] = x.x;
-            cd[4 * r8 + 1] = x.y;
-            cd[4 * r8 + 2] = x.z;
-            cd[4 * r8 + 3] = x.w;
+        for (int k = 0; k < kRowsPerChunk; k++) {
+            const int64_t ro = g0 + ((cb + k) << 10) + 16 * (int64_t)l;
+            x[k] = (u32x4){0, 0, 0, 0};
+            if (cb + k < niter && ro + 16 > 21) x[k] = ld16(p + ro);
         }
 #pragma unroll
-        for (int r8 = 0; r8 < ROWS; r8++) {
-            if (cb + r8 < niter) {
-                const int64_t ro = g0 + ((cb + r8) << 10) + 16 * (int64_t)l;
-                u32x4 x = {cd[4 * r8], cd[4 * r8 + 1], cd[4 * r8 + 2], cd[4 * r8 + 3]};
-                if (g0 + ((cb + r8) << 10) < kHeaderSize) {
-                    // header image merge for bytes < 61 (rows 0 and, when the
+        for (int k = 0; k < kRowsPerChunk; k++) {
+            if (cb + k < niter) {
+                if (walk) reinterpret_cast<u32x4*>(stg)[k * 64 + l] = x[k];
+                const int64_t ro = g0 + ((cb + k) << 10) + 16 * (int64_t)l;
+                u32x4 y = x[k];
+                if (g0 + ((cb + k) << 10) < kHeaderSize) {
+                    // header image merge for bytes < 61 (row 0 and, when the
                     // grid origin is below -963, row 1)
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
@@ -616,23 +290,26 @@ __device__ void process_batch(const uint32_t* __restrict__ sT, const rpgpu_batch
                             keep = 0;
                         else
                             keep = 0xffffffffu << (8 * (uint32_t)(kHeaderSize - o4));
-                        const uint32_t raw = q == 0 ? x.x : q == 1 ? x.y : q == 2 ? x.z : x.w;
+                        const uint32_t raw = q == 0 ? y.x : q == 1 ? y.y : q == 2 ? y.z : y.w;
                         const uint32_t v = (raw & keep) | (o4 >= kHeaderSize ? 0u : im);
-                        if (q == 0) x.x = v;
-                        if (q == 1) x.y = v;
-                        if (q == 2) x.z = v;
-                        if (q == 3) x.w = v;
+                        if (q == 0) y.x = v;
+                        if (q == 1) y.y = v;
+                        if (q == 2) y.z = v;
+                        if (q == 3) y.w = v;
                     }
                 }
-                x.x ^= c;
-                c = crc_block(sV, x);
+                y.x ^= c;
+                c = crc_block(sV, y);
             }
         }
-        if (w.state != WS_DONE) {
+        if (walk && !whole) {
+            // too large to stage whole: exact walk chunk by chunk
+            wave_lds_sync();
             const int64_t cbase = g0 + (cb << 10);
-            int64_t hi = cbase + ((int64_t)ROWS << 10);
+            int64_t hi = cbase + ((int64_t)kRowsPerChunk << 10);
             if (hi > n) hi = n;
-            walker_run(w, cd, cbase, hi, em);
+            walker_run(w, stg, cbase, hi, em);
+            wave_lds_sync();
         }
     }
     c = combine64(sT + kOffW, c);
@@ -646,13 +323,20 @@ __device__ void process_batch(const uint32_t* __restrict__ sT, const rpgpu_batch
     } else if (codec > 4) {
         r.verdict = RPGPU_V_BAD_CODEC_THROW;
     } else if (walk) {
-        r.verdict = w.verdict;
-        if (em.index) {
-            const uint32_t cnt = w.cnt < cap ? w.cnt : cap;
+        int32_t verdict;
+        uint32_t cnt;
+        if (whole) {
+            wave_lds_sync();
+            if (!fast_walk(stg, g0, n, r.h.record_count, cap, em, &verdict, &cnt))
+                slow_walk_whole(stg, g0, n, r.h.record_count, cap, em, &verdict, &cnt);
+        } else {
+            cnt = w.cnt < cap ? w.cnt : cap;
             const uint32_t rem = cnt & 63u;
-            if (rem) flush_entries(w, em, rem, cnt - rem);
-            r.index_count = cnt;
+            if (em.index && rem) flush_entries(w, em, rem, cnt - rem);
+            verdict = w.verdict;
         }
+        r.verdict = verdict;
+        if (em.index) r.index_count = cnt;
     }
     write_result(res, r);
 }
@@ -665,11 +349,12 @@ __global__ __launch_bounds__(kValidateThreads) void validate_kernel(
     const uint32_t* __restrict__ local_first, const uint32_t* __restrict__ caps,
     const uint64_t* __restrict__ block_base, uint64_t index_cap, const uint32_t* __restrict__ tables) {
     __shared__ __attribute__((aligned(16))) uint32_t sT[kTableWords];
+    __shared__ __attribute__((aligned(16))) uint32_t sStage[kWavesPerBlock * kStageWords];
     load_tables(sT, tables);
     const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t waves_per_block = blockDim.x >> 6;
-    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * waves_per_block + wave);
-    const uint32_t nw = gridDim.x * waves_per_block;
+    uint32_t* stg = sStage + wave * kStageWords;
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + wave);
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
     for (uint32_t b = gw; b < n; b += nw) {
         const rpgpu_batch_desc d = descs[b];
         const uint64_t first = block_base[b / kScanBlock] + local_first[b];
@@ -677,7 +362,7 @@ __global__ __launch_bounds__(kValidateThreads) void validate_kernel(
         uint64_t cap = caps[b];
         if (first >= index_cap) cap = 0;
         else if (first + cap > index_cap) cap = index_cap - first;
-        process_batch<kRowsPerChunk>(sT, d, data, res + b, index, (uint32_t)first, (uint32_t)cap);
+        process_batch(sT, stg, d, data, res + b, index, (uint32_t)first, (uint32_t)cap);
     }
 }
 
@@ -722,7 +407,6 @@ __global__ __launch_bounds__(kScanBlock) void caps_kernel(const rpgpu_batch_desc
     const uint32_t i = blockIdx.x * kScanBlock + threadIdx.x;
     uint32_t cap = 0;
     if (i < n) cap = index_cap(descs[i], data);
-    // wave inclusive scan
     const uint32_t l = lane_id();
     uint32_t x = cap;
 #pragma unroll
@@ -746,7 +430,7 @@ __global__ __launch_bounds__(kScanBlock) void caps_kernel(const rpgpu_batch_desc
     }
 }
 
-// exclusive scan of block sums (single workgroup), writes total at [nb]
+// exclusive scan of block sums (single workgroup), total into *total_out
 __global__ __launch_bounds__(1024) void block_scan_kernel(uint64_t* __restrict__ block_sum, uint32_t nb,
                                                           uint64_t* __restrict__ total_out) {
     __shared__ uint64_t part[1024];
@@ -784,9 +468,8 @@ __global__ __launch_bounds__(kValidateThreads) void crc_ranges_kernel(
     load_tables(sT, tables);
     const uint32_t l = lane_id();
     const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t waves_per_block = blockDim.x >> 6;
-    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * waves_per_block + wave);
-    const uint32_t nw = gridDim.x * waves_per_block;
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + wave);
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
     const uint32_t* sV = sT + kOffV;
     for (uint32_t i = gw; i < n; i += nw) {
         const uint8_t* base = data + offs[i];
@@ -819,7 +502,6 @@ __global__ __launch_bounds__(kValidateThreads) void crc_ranges_kernel(
 #pragma unroll
                         for (int q = 0; q < 4; q++) {
                             const int64_t o4 = ro + 4 * q;
-                            // xor init into bytes [0,4): byte j of dword at o4 is offset o4+j
                             uint32_t m = 0;
 #pragma unroll
                             for (int j = 0; j < 4; j++) {
@@ -843,11 +525,7 @@ __global__ __launch_bounds__(kValidateThreads) void crc_ranges_kernel(
     }
 }
 
-}  // namespace rpgpu
-
 // ------------------------------------------------------------ launchers
-namespace rpgpu {
-
 // scratch layout: caps[n] u32 | local_first[n] u32 | block_sum[nb] u64
 static void scratch_parts(void* d_scratch, uint32_t n, uint32_t** caps, uint32_t** local_first,
                           uint64_t** block_sum) {
@@ -879,7 +557,7 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
     uint32_t *caps, *local_first;
     uint64_t* block_sum;
     scratch_parts(const_cast<void*>(d_scratch), n, &caps, &local_first, &block_sum);
-    const uint32_t need = (n + (kValidateThreads / 64) - 1) / (kValidateThreads / 64);
+    const uint32_t need = (n + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint32_t g = (uint32_t)grid < need ? (uint32_t)grid : need;
     validate_kernel<<<g, kValidateThreads, 0, s>>>(d_descs, n, d_data, d_res, d_index, local_first, caps,
                                                     block_sum, index_cap, d_tables);
@@ -899,7 +577,7 @@ hipError_t launch_crc_ranges(const uint8_t* d_data, const uint64_t* d_off, const
                              const uint32_t* d_seed, uint32_t n, uint32_t* d_out, const uint32_t* d_tables,
                              int grid, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const uint32_t need = (n + (kValidateThreads / 64) - 1) / (kValidateThreads / 64);
+    const uint32_t need = (n + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint32_t g = (uint32_t)grid < need ? (uint32_t)grid : need;
     crc_ranges_kernel<<<g, kValidateThreads, 0, s>>>(d_data, d_off, d_len, d_seed, n, d_out, d_tables);
     return hipGetLastError();

@@ -7,8 +7,8 @@
 //           invertible because the polynomial has a non-zero constant term);
 //   V[j]  = S_{j+1008} o T0 for j = 0..15  (slice-by-16 with the 1008-byte
 //           gap between one lane's consecutive blocks folded in);
-//   W[s]  = S_{-16*2^s} split into 4 byte tables (butterfly combine);
-//   H     = S_{-960} (header-CRC window correction);
+//   W[s]  = S_{-16*2^s} split into 8 nibble tables (butterfly combine);
+//   H     = S_{-960} as 8 nibble tables (header-CRC window correction);
 //   T0    = the plain byte table.
 #include <stdint.h>
 #include <string.h>
@@ -39,11 +39,11 @@ uint32_t apply_basis(const uint32_t basis[32], uint32_t v) {
         if (v >> i & 1) r ^= basis[i];
     return r;
 }
-void byte_tables(int64_t k, uint32_t* out /* 4 x 256 */) {
+void nibble_tables(int64_t k, uint32_t* out /* 8 x 16 */) {
     uint32_t basis[32];
     shift_basis(k, basis);
-    for (int j = 0; j < 4; j++)
-        for (uint32_t b = 0; b < 256; b++) out[j * 256 + b] = apply_basis(basis, b << (8 * j));
+    for (int j = 0; j < 8; j++)
+        for (uint32_t v = 0; v < 16; v++) out[j * 16 + v] = apply_basis(basis, v << (4 * j));
 }
 }  // namespace
 
@@ -60,8 +60,8 @@ void build_tables(uint32_t* out) {
         shift_basis(j + 1008, basis);
         for (uint32_t b = 0; b < 256; b++) out[kOffV + j * 256 + b] = apply_basis(basis, t0[b]);
     }
-    for (int s = 0; s < 6; s++) byte_tables(-16ll * (1ll << s), out + kOffW + s * 1024);
-    byte_tables(-960, out + kOffH);
+    for (int s = 0; s < 6; s++) nibble_tables(-16ll * (1ll << s), out + kOffW + s * 128);
+    nibble_tables(-960, out + kOffH);
 }
 
 }  // namespace rpgpu
