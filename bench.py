@@ -17,6 +17,7 @@ Prints ONE JSON line on rank 0 (contract in the task statement).
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -214,6 +215,14 @@ def main() -> int:
                      "algorithmic_bytes_per_launch": int(alg_bytes)},
         "cpu_baseline": None,
     }
+    L = abi.lib()
+    if hasattr(L, "rpgpu_diag_stamps"):  # diagnostics build only (scripts/diag_build.sh)
+        st = (C.c_ulonglong * 8)()
+        torch.cuda.synchronize()
+        L.rpgpu_diag_stamps(st)
+        per = float(n) * (args.warmup + args.steps)
+        out["diag_cycles_per_batch"] = {k: round(st[i] / per, 1) for i, k in enumerate(
+            ["header", "stage", "crc", "combine", "walk", "loop"])}
     prof = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(prof):
         try:

@@ -11,6 +11,8 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <stdlib.h>
+
 #include <vector>
 
 #include "rpgpu.h"
@@ -111,8 +113,14 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
         return nullptr;
     }
     c->cu_count = prop.multiProcessorCount;
-    // one 8-wave workgroup per CU: CRC tables + 8 x 16 KiB staging fill the LDS
-    c->grid = c->cu_count;
+    // kBlocksPerCU 4-wave workgroups per CU (RPGPU_BLOCKS_PER_CU overrides,
+    // for tuning runs)
+    int bpc = rpgpu::kBlocksPerCU;
+    if (const char* e = getenv("RPGPU_BLOCKS_PER_CU")) {
+        const int v = atoi(e);
+        if (v >= 1 && v <= 32) bpc = v;
+    }
+    c->grid = c->cu_count * bpc;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return nullptr;

@@ -14,19 +14,22 @@ constexpr int32_t kHeaderSize = RPGPU_HEADER_SIZE;  // model/record.h:527-540
 constexpr uint32_t kCopyLimit = 64u << 20;
 constexpr int64_t kHcountLimit = 1ll << 20;
 
-// CRC table blob (uint32 words): see rpgpu_tables.cpp
-constexpr int kOffV = 0;                 // 16 x 256: slice-by-16, pre-shifted 1008 B
-constexpr int kOffW = 16 * 256;          // 6 x 8 x 16: x^(-8*16*2^s), nibble tables
+// CRC table blob (uint32 words): see rpgpu_tables.cpp.  Every table that is
+// indexed per lane has 16 entries, so a wave's lookups never conflict on an
+// LDS bank (16 entries sit in 16 distinct banks).
+constexpr int kOffN = 0;                 // 32 x 16: block nibble tables, pre-shifted 1008 B
+constexpr int kOffW = kOffN + 32 * 16;   // 6 x 8 x 16: x^(-8*16*2^s), nibble tables
 constexpr int kOffH = kOffW + 6 * 128;   // 8 x 16: x^(-8*960), nibble tables
-constexpr int kOffT0 = kOffH + 128;      // 256: plain byte table
-constexpr int kTableWords = kOffT0 + 256;
+constexpr int kOffT0 = kOffH + 128;      // 256: plain byte table (ranges shorter than 4 B)
+constexpr int kOffP = kOffT0 + 256;      // 16 x 8 x 16: x^(-8*p), p = 0..15 (row-grid pad)
+constexpr int kTableWords = kOffP + 16 * 128;
 static_assert(kTableWords % 4 == 0, "table blob is copied as 16-byte words");
 
-constexpr int kValidateThreads = 512;  // 8 waves per workgroup, one workgroup per CU
+constexpr int kValidateThreads = 256;  // 4 waves per workgroup
 constexpr int kWavesPerBlock = kValidateThreads / 64;
-constexpr int kRowsPerChunk = 16;      // 16 x 1 KiB rows per wave per chunk
-constexpr uint32_t kStageBytes = kRowsPerChunk * 1024u;
-constexpr uint32_t kStageWords = kStageBytes / 4 + 16;  // + 64 B read-ahead pad
+constexpr int kBlocksPerCU = 4;        // default grid: 16 waves per CU
+constexpr int kRowsPerChunk = 16;      // 16 x 1 KiB rows in flight per wave
+constexpr int kGroup = 64;             // batches per wave between record walks (one per lane)
 constexpr int kScanBlock = 1024;
 
 void build_tables(uint32_t* out /* kTableWords */);

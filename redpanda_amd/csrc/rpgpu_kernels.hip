@@ -1,34 +1,55 @@
 // rpgpu_kernels.hip — CDNA4 (gfx950) kernels of the record-batch engine.
 //
-// One wavefront owns one batch at a time (grid-stride over the arena); one
-// 8-wave workgroup per CU shares the CRC tables (20.5 KiB) and gives each
-// wave a 16 KiB LDS staging buffer.
+// validate_kernel: one wavefront owns one batch at a time (grid-stride over
+// the arena, 16 waves per CU).  Two phases per group of 64 batches:
 //
-// CRC32C layout ("strided rows").  The Kafka CRC covers batch bytes
-// [21, n) (kafka_batch_adapter.cc:99-134).  That region is cut into 16-byte
-// blocks counted from its END, and 64 consecutive blocks form a 1 KiB "row";
-// lane l of row t owns block r = 64t + 63 - l, so every row is one coalesced
-// 1 KiB load (16 B per lane).  Each lane keeps its own CRC state over the
-// blocks it owns; because those blocks are 1008 bytes apart, the slice-by-16
-// tables are pre-multiplied by x^(8*1008) (shift by 1008 zero bytes), so a
-// lane advances with exactly 16 table lookups per 16 bytes.  At the end the
-// 64 lane states are folded by a 6-step butterfly whose step s applies the
-// constant shift x^(-8*16*2^s) (tables W).  The CRC init value is folded into
-// the first four bytes of the message (standard reflected-CRC identity) and
-// bytes before the region are zeroed, so arbitrary alignment costs nothing.
+// (1) CRC32C, all 64 lanes on one batch ("strided rows").  The Kafka CRC
+// covers batch bytes [21, n) (kafka_batch_adapter.cc:99-134).  The region is
+// extended to a 16-byte aligned END (the extension is zeroed and removed at
+// the end with the map x^(-8*pad), tables P) and cut into 16-byte blocks
+// counted from that end; 64 consecutive blocks form a 1 KiB "row", lane l of
+// row t owning block r = 64t + 63 - l, so every row is one aligned,
+// coalesced 1 KiB load (16 B per lane).  Each lane keeps its own CRC state
+// over the blocks it owns; they are 1008 bytes apart, so the tables are
+// pre-multiplied by x^(8*1008) and a lane advances with 32 nibble lookups per
+// 16 bytes (16-entry tables: no LDS bank conflicts).  A 6-step butterfly
+// folds the 64 lane states (tables W).  The CRC init is folded into the
+// first four bytes of the message and bytes before the region are zeroed.
+// Header bytes [21, 61) are taken from an "image" built from the parsed
+// header (big-endian, as crc_record_batch_header hashes them,
+// record_utils.cc:68-80), so one loop serves wire and on-disk batches.
+// The next batch's rows are loaded into the registers each row frees as it
+// is checksummed, so 16 KiB per wave stay in flight.
 //
-// Header bytes [21, 61) are taken from a per-batch "image" built from the
-// parsed header (big-endian, as crc_record_batch_header hashes them,
-// record_utils.cc:68-80), which makes the same loop serve wire batches and
-// on-disk (little-endian) batches.
-//
-// Record walk (rpgpu_walk.h): the rows are also written to the wave's LDS
-// staging buffer; batches of up to 16 rows are walked after the CRC by the
-// lane-parallel fast walk, larger ones chunk by chunk by the exact walker.
+// (2) Record walk (rpgpu_walk.h), one lane per batch of the group.
 #include "rpgpu_device.h"
 #include "rpgpu_walk.h"
 
 namespace rpgpu {
+
+// Diagnostics build only (scripts/diag_build.sh STAMPS): per-phase wave
+// cycles from s_memtime, summed over all waves into g_stamps.
+#ifdef RPGPU_DIAG_STAMPS
+__device__ unsigned long long g_stamps[8];
+struct Stamps {
+    uint64_t st[8];
+    uint64_t prev;
+};
+#define DIAG_PARAM , Stamps& sp
+#define DIAG_PASS , sp
+#define STAMP(i)                                          \
+    do {                                                  \
+        const uint64_t _t = __builtin_amdgcn_s_memtime(); \
+        sp.st[i] += _t - sp.prev;                         \
+        sp.prev = _t;                                     \
+    } while (0)
+#else
+#define DIAG_PARAM
+#define DIAG_PASS
+#define STAMP(i) \
+    do {         \
+    } while (0)
+#endif
 
 // Parsed record_batch_header (model/record.h:356-440), wave-uniform.
 struct Header {
@@ -91,21 +112,116 @@ __device__ __forceinline__ uint32_t header_crc_vec(const uint32_t* sT, const Img
     for (int j = 0; j < 4; j++) {
         if (l == (uint32_t)j) blk = (u32x4){win[4 * j], win[4 * j + 1], win[4 * j + 2], win[4 * j + 3]};
     }
-    uint32_t c = crc_block(sT + kOffV, blk);
+    uint32_t c = crc_block(sT + kOffN, blk);
     const uint32_t* sW = sT + kOffW;
-#pragma unroll
-    for (int s = 0; s < 2; s++) {
-        uint32_t t = __shfl_down(c, 1 << s, 64);
-        c ^= apply8(sW + s * 128, t);
-    }
+    c ^= apply8(sW + 0 * 128, row_shl<1>(c));
+    c ^= apply8(sW + 1 * 128, row_shl<2>(c));
     c = apply8(sT + kOffH, c);
     return ~rdl(c, 0);
 }
 
-__device__ void process_batch(const uint32_t* __restrict__ sT, uint32_t* __restrict__ stg,
-                              const rpgpu_batch_desc& d, const uint8_t* __restrict__ data,
-                              rpgpu_batch_result* __restrict__ res, rpgpu_record_index* __restrict__ index,
-                              uint32_t index_first, uint32_t cap) {
+// Row geometry of the CRC region [21, n) of a batch starting at absolute
+// address `at`: the end is extended by `pad` bytes to a 16-byte boundary;
+// niter 1 KiB rows end there, row k starts at batch offset g0 + 1024 k.
+struct Geom {
+    int64_t niter, g0;
+    uint32_t pad;
+};
+__device__ __forceinline__ Geom geometry(uint64_t at, int64_t n) {
+    const uint32_t pad = (uint32_t)(0 - (at + (uint64_t)n)) & 15u;
+    const int64_t ne = n + pad;
+    const int64_t nblocks = (ne - 21 + 15) >> 4;
+    const int64_t niter = (nblocks + 63) >> 6;
+    return Geom{niter, ne - (niter << 10), pad};
+}
+
+// One batch's first chunk of rows and its 64-byte header window, loaded
+// ahead of time with the geometry implied by the descriptor length (the
+// batch is re-loaded in the rare case its header trims it shorter).
+struct Prefetch {
+    u32x4 x[kRowsPerChunk];
+    uint32_t hv;
+    Geom gm;
+};
+
+// Rows are read through a buffer resource based at the batch start: lanes
+// whose block starts before the batch (negative offset, out of range as an
+// unsigned offset) and rows past the region (offset 2^31) read zeros
+// without touching memory.  The load is always issued, so the number of
+// loads per batch is fixed and the compiler waits for one row with a counted
+// vmcnt instead of draining every row in flight.  Batches are shorter than
+// 2^31 bytes (Kafka's batch_length is an int32; RPGPU_MAX_BATCH_BYTES).
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t batch_rsrc(const uint8_t* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p), 0, 0x7ffffff0, 0x00020000);
+}
+__device__ __forceinline__ u32x4 load_row(__amdgpu_buffer_rsrc_t rs, const Geom& gm, int64_t row, uint32_t l) {
+    const int32_t rb = row < gm.niter ? (int32_t)(gm.g0 + (row << 10)) : (int32_t)0x80000000;
+    const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, rb + (int32_t)(16 * l), 0, 0);
+    return (u32x4){(uint32_t)v.x, (uint32_t)v.y, (uint32_t)v.z, (uint32_t)v.w};
+}
+
+__device__ __forceinline__ void load_rows(u32x4 (&x)[kRowsPerChunk], __amdgpu_buffer_rsrc_t rs, const Geom& gm,
+                                          int64_t cb, uint32_t l) {
+#pragma unroll
+    for (int k = 0; k < kRowsPerChunk; k++) x[k] = load_row(rs, gm, cb + k, l);
+}
+
+__device__ __forceinline__ Geom desc_geometry(const rpgpu_batch_desc& d, const uint8_t* data) {
+    return d.length >= (uint32_t)kHeaderSize ? geometry((uint64_t)(data + d.offset), d.length) : Geom{0, 0, 0};
+}
+
+// Row block at batch offset ro0 + 16*lane with bytes [0, 61) replaced by the
+// header image (zero below 21, big-endian fields in [21, 61), CRC init folded
+// into [21, 25)); rows starting at or after 61 pass through.
+__device__ __forceinline__ u32x4 merge_header(u32x4 y, int64_t ro0, uint32_t v_img, uint32_t l) {
+    if (ro0 >= kHeaderSize) return y;
+    const int64_t ro = ro0 + 16 * (int64_t)l;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int64_t o4 = ro + 4 * q;
+        const uint32_t im = img_dword(v_img, o4);
+        uint32_t keep;  // raw bytes at offsets >= 61
+        if (o4 >= kHeaderSize)
+            keep = 0xffffffffu;
+        else if (o4 + 4 <= kHeaderSize)
+            keep = 0;
+        else
+            keep = 0xffffffffu << (8 * (uint32_t)(kHeaderSize - o4));
+        const uint32_t raw = q == 0 ? y.x : q == 1 ? y.y : q == 2 ? y.z : y.w;
+        const uint32_t v = (raw & keep) | (o4 >= kHeaderSize ? 0u : im);
+        if (q == 0) y.x = v;
+        if (q == 1) y.y = v;
+        if (q == 2) y.z = v;
+        if (q == 3) y.w = v;
+    }
+    return y;
+}
+
+// last block of the region (lane 63 of the last row): zero the pad bytes
+__device__ __forceinline__ u32x4 mask_pad(u32x4 y, uint32_t pad, uint32_t l) {
+    const uint32_t keep = 16u - pad;  // bytes of the block inside the region
+    uint32_t m[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        m[q] = keep >= 4u * q + 4 ? 0xffffffffu : (keep <= 4u * q ? 0u : (1u << (8 * (keep - 4 * q))) - 1);
+    if (l == 63) {
+        y.x &= m[0];
+        y.y &= m[1];
+        y.z &= m[2];
+        y.w &= m[3];
+    }
+    return y;
+}
+
+// Checksums one batch whose header window and first rows are in `pf` and,
+// as the rows free their registers, loads the next batch's rows into them.
+// A batch that needs a record walk becomes lane j's WalkJob.
+__device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, const rpgpu_batch_desc& d,
+                                              uint32_t b, const uint8_t* __restrict__ data,
+                                              rpgpu_batch_result* __restrict__ res, uint32_t index_first,
+                                              uint32_t cap, Prefetch& pf, const rpgpu_batch_desc& nd,
+                                              bool has_next, WalkJob& J, uint32_t j DIAG_PARAM) {
     const uint32_t l = lane_id();
     const uint8_t* p = data + d.offset;
     const uint32_t len = d.length;
@@ -116,23 +232,25 @@ __device__ void process_batch(const uint32_t* __restrict__ sT, uint32_t* __restr
     r.index_first = index_first;
     r.index_count = 0;
 
-    // ---- 64-byte header window (RPGPU_ARENA_TAIL_PAD keeps it readable)
-    const uint32_t hv = (l < 16) ? ld4(p + 4 * l) : 0u;
+    // ---- 64-byte header window; the next batch's goes in flight at once
+    const uint32_t hv = pf.hv;
     Img64 H;
 #pragma unroll
-    for (int j = 0; j < 16; j++) H.w[j] = rdl(hv, j);
+    for (int i = 0; i < 16; i++) H.w[i] = rdl(hv, i);
+    Geom ngm{0, 0, 0};
+    // always issued (lanes 16..63 repeat the window): a fixed load count
+    // keeps the compiler's vmcnt bookkeeping exact
+    const __amdgpu_buffer_rsrc_t nrs = batch_rsrc(data + (has_next ? nd.offset : 0));
+    pf.hv = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(nrs, (int32_t)(4 * (l & 15)), 0, 0);
+    if (has_next) ngm = desc_geometry(nd, data);
 
     Img64 D;  // little-endian disk header image (CRC'd bytes [4, 61))
     D.clear();
     int64_t n;  // end of the Kafka-CRC region (trimmed batch length)
     bool body_trunc = false;
+    bool fail = false;
     if (d.format == RPGPU_FMT_KAFKA_WIRE) {
         // kafka_batch_adapter::adapt / read_header (kafka_batch_adapter.cc:32-198)
-        if (len < 12) {
-            r.verdict = RPGPU_V_TOO_SMALL;
-            write_result(res, r);
-            return;
-        }
         const int32_t bl = (int32_t)H.get_be(8, 4);
         const uint64_t blen = (uint64_t)(int64_t)bl + 12u;
         if (blen <= (uint64_t)len) {
@@ -141,93 +259,98 @@ __device__ void process_batch(const uint32_t* __restrict__ sT, uint32_t* __restr
             n = len;
             body_trunc = true;
         }
-        if (n < 17) {
+        if (len < 12) {
+            r.verdict = RPGPU_V_TOO_SMALL;
+            fail = true;
+        } else if (n < 17) {
             r.verdict = RPGPU_V_HDR_TRUNC_THROW;
-            write_result(res, r);
-            return;
-        }
-        if ((int8_t)H.byte(16) != 2) {
+            fail = true;
+        } else if ((int8_t)H.byte(16) != 2) {
             r.verdict = RPGPU_V_BAD_MAGIC;
-            write_result(res, r);
-            return;
-        }
-        if (n < kHeaderSize) {
+            fail = true;
+        } else if (n < kHeaderSize) {
             r.verdict = RPGPU_V_HDR_TRUNC_THROW;
-            write_result(res, r);
-            return;
+            fail = true;
+        } else {
+            r.h.size_bytes = (int32_t)((uint32_t)bl + 12u);
+            r.h.base_offset = (int64_t)H.get_be(0, 8);
+            r.h.type = 1;  // record_batch_type::raft_data
+            r.h.crc = (int32_t)H.get_be(17, 4);
+            r.h.attrs = (int16_t)H.get_be(21, 2);
+            r.h.last_offset_delta = (int32_t)H.get_be(23, 4);
+            r.h.first_ts = (int64_t)H.get_be(27, 8);
+            r.h.max_ts = (int64_t)H.get_be(35, 8);
+            r.h.producer_id = (int64_t)H.get_be(43, 8);
+            r.h.producer_epoch = (int16_t)H.get_be(51, 2);
+            r.h.base_sequence = (int32_t)H.get_be(53, 4);
+            r.h.record_count = (int32_t)H.get_be(57, 4);
+            D.put_le(4, (uint32_t)r.h.size_bytes, 4);
+            D.put_le(8, (uint64_t)r.h.base_offset, 8);
+            D.put_le(16, 1, 1);
+            D.put_le(17, (uint32_t)r.h.crc, 4);
+            D.put_le(21, (uint16_t)r.h.attrs, 2);
+            D.put_le(23, (uint32_t)r.h.last_offset_delta, 4);
+            D.put_le(27, (uint64_t)r.h.first_ts, 8);
+            D.put_le(35, (uint64_t)r.h.max_ts, 8);
+            D.put_le(43, (uint64_t)r.h.producer_id, 8);
+            D.put_le(51, (uint16_t)r.h.producer_epoch, 2);
+            D.put_le(53, (uint32_t)r.h.base_sequence, 4);
+            D.put_le(57, (uint32_t)r.h.record_count, 4);
         }
-        r.h.size_bytes = (int32_t)((uint32_t)bl + 12u);
-        r.h.base_offset = (int64_t)H.get_be(0, 8);
-        r.h.type = 1;  // record_batch_type::raft_data
-        r.h.crc = (int32_t)H.get_be(17, 4);
-        r.h.attrs = (int16_t)H.get_be(21, 2);
-        r.h.last_offset_delta = (int32_t)H.get_be(23, 4);
-        r.h.first_ts = (int64_t)H.get_be(27, 8);
-        r.h.max_ts = (int64_t)H.get_be(35, 8);
-        r.h.producer_id = (int64_t)H.get_be(43, 8);
-        r.h.producer_epoch = (int16_t)H.get_be(51, 2);
-        r.h.base_sequence = (int32_t)H.get_be(53, 4);
-        r.h.record_count = (int32_t)H.get_be(57, 4);
-        D.put_le(4, (uint32_t)r.h.size_bytes, 4);
-        D.put_le(8, (uint64_t)r.h.base_offset, 8);
-        D.put_le(16, 1, 1);
-        D.put_le(17, (uint32_t)r.h.crc, 4);
-        D.put_le(21, (uint16_t)r.h.attrs, 2);
-        D.put_le(23, (uint32_t)r.h.last_offset_delta, 4);
-        D.put_le(27, (uint64_t)r.h.first_ts, 8);
-        D.put_le(35, (uint64_t)r.h.max_ts, 8);
-        D.put_le(43, (uint64_t)r.h.producer_id, 8);
-        D.put_le(51, (uint16_t)r.h.producer_epoch, 2);
-        D.put_le(53, (uint32_t)r.h.base_sequence, 4);
-        D.put_le(57, (uint32_t)r.h.record_count, 4);
     } else {
         // storage::continuous_batch_parser read_header_impl (parser.cc:155-216)
+        n = 0;
         if (len < kHeaderSize) {
             r.verdict = RPGPU_V_STREAM_SHORT;
-            write_result(res, r);
-            return;
-        }
-        uint32_t any = 0;
+            fail = true;
+        } else {
+            uint32_t any = 0;
 #pragma unroll
-        for (int j = 0; j < 15; j++) any |= H.w[j];
-        any |= H.w[15] & 0xffu;  // byte 60 only (61..63 are past the header)
-        if (any == 0) {
-            r.verdict = RPGPU_V_FALLOCATED_ZERO;
-            write_result(res, r);
-            return;
-        }
+            for (int i = 0; i < 15; i++) any |= H.w[i];
+            any |= H.w[15] & 0xffu;  // byte 60 only (61..63 are past the header)
+            if (any == 0) {
+                r.verdict = RPGPU_V_FALLOCATED_ZERO;
+                fail = true;
+            } else {
 #pragma unroll
-        for (int j = 0; j < 16; j++) D.w[j] = H.w[j];
-        D.w[15] &= 0xffu;
-        r.h.size_bytes = (int32_t)H.get_le(4, 4);
-        r.h.base_offset = (int64_t)H.get_le(8, 8);
-        r.h.type = (int8_t)H.byte(16);
-        r.h.crc = (int32_t)H.get_le(17, 4);
-        r.h.attrs = (int16_t)H.get_le(21, 2);
-        r.h.last_offset_delta = (int32_t)H.get_le(23, 4);
-        r.h.first_ts = (int64_t)H.get_le(27, 8);
-        r.h.max_ts = (int64_t)H.get_le(35, 8);
-        r.h.producer_id = (int64_t)H.get_le(43, 8);
-        r.h.producer_epoch = (int16_t)H.get_le(51, 2);
-        r.h.base_sequence = (int32_t)H.get_le(53, 4);
-        r.h.record_count = (int32_t)H.get_le(57, 4);
-        n = (int64_t)r.h.size_bytes;
+                for (int i = 0; i < 16; i++) D.w[i] = H.w[i];
+                D.w[15] &= 0xffu;
+                r.h.size_bytes = (int32_t)H.get_le(4, 4);
+                r.h.base_offset = (int64_t)H.get_le(8, 8);
+                r.h.type = (int8_t)H.byte(16);
+                r.h.crc = (int32_t)H.get_le(17, 4);
+                r.h.attrs = (int16_t)H.get_le(21, 2);
+                r.h.last_offset_delta = (int32_t)H.get_le(23, 4);
+                r.h.first_ts = (int64_t)H.get_le(27, 8);
+                r.h.max_ts = (int64_t)H.get_le(35, 8);
+                r.h.producer_id = (int64_t)H.get_le(43, 8);
+                r.h.producer_epoch = (int16_t)H.get_le(51, 2);
+                r.h.base_sequence = (int32_t)H.get_le(53, 4);
+                r.h.record_count = (int32_t)H.get_le(57, 4);
+                n = (int64_t)r.h.size_bytes;
+            }
+        }
     }
-    r.crc_expected = (uint32_t)r.h.crc;
-
     const bool is_disk = d.format != RPGPU_FMT_KAFKA_WIRE;
-    if ((d.ops & RPGPU_OP_HDRCRC) || is_disk) r.header_crc = header_crc_vec(sT, D);
-    if (is_disk) {
-        if (r.header_crc != H.w[0]) {
-            r.verdict = RPGPU_V_HDR_CRC_MISMATCH;
-            write_result(res, r);
-            return;
+    if (!fail) {
+        r.crc_expected = (uint32_t)r.h.crc;
+        if ((d.ops & RPGPU_OP_HDRCRC) || is_disk) r.header_crc = header_crc_vec(sT, D);
+        if (is_disk) {
+            if (r.header_crc != H.w[0]) {
+                r.verdict = RPGPU_V_HDR_CRC_MISMATCH;
+                fail = true;
+            } else if (r.h.size_bytes < kHeaderSize || (int64_t)r.h.size_bytes > (int64_t)len) {
+                r.verdict = RPGPU_V_STREAM_SHORT;
+                fail = true;
+            }
         }
-        if (r.h.size_bytes < kHeaderSize || (int64_t)r.h.size_bytes > (int64_t)len) {
-            r.verdict = RPGPU_V_STREAM_SHORT;
-            write_result(res, r);
-            return;
-        }
+    }
+    if (fail) {
+        // nothing of this batch is checksummed: just move the next one's rows
+        load_rows(pf.x, nrs, ngm, 0, l);
+        pf.gm = ngm;
+        write_result(res + b, r);
+        return;
     }
 
     // ---- body-CRC image: bytes [21, 61) big-endian (record_utils.cc:68-80),
@@ -246,124 +369,132 @@ __device__ void process_batch(const uint32_t* __restrict__ sT, uint32_t* __restr
     B.w[6] ^= 0x000000ffu;  // byte 24
     uint32_t v_img = 0;
 #pragma unroll
-    for (int j = 0; j < 16; j++) v_img = (l == (uint32_t)j) ? B.w[j] : v_img;
-
-    const uint8_t codec = (uint8_t)(r.h.attrs & 7);
-    const bool walk = !body_trunc && codec == 0 && (d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX));
-    EmitCtx em{index + index_first, r.h.base_offset, r.h.first_ts, (d.ops & RPGPU_OP_INDEX) != 0};
+    for (int i = 0; i < 16; i++) v_img = (l == (uint32_t)i) ? B.w[i] : v_img;
 
     // ---- rows over the CRC region [21, n)
-    const int64_t nblocks = (n - 21 + 15) >> 4;
-    const int64_t niter = (nblocks + 63) >> 6;
-    const int64_t g0 = n - (niter << 10);
-    const bool whole = niter <= kRowsPerChunk;  // batch fits the staging buffer
-    // exact walker state for batches walked chunk by chunk (large batches only)
-    Walker w;
-    if (walk && !whole) walker_init(w, n, r.h.record_count, cap, true);
-    const uint32_t* sV = sT + kOffV;
+    const Geom gm = geometry((uint64_t)p, n);
+    const int64_t niter = gm.niter;
+    const bool pf_ok = pf.gm.niter == niter && pf.gm.g0 == gm.g0;  // prefetch geometry matches
+    const uint32_t* sN = sT + kOffN;
+    const __amdgpu_buffer_rsrc_t rs = batch_rsrc(p);
     uint32_t c = 0;
+    STAMP(0);
+    if (!pf_ok) load_rows(pf.x, rs, gm, 0, l);
     for (int64_t cb = 0; cb < niter; cb += kRowsPerChunk) {
-        u32x4 x[kRowsPerChunk];
-#pragma unroll
-        for (int k = 0; k < kRowsPerChunk; k++) {
-            const int64_t ro = g0 + ((cb + k) << 10) + 16 * (int64_t)l;
-            x[k] = (u32x4){0, 0, 0, 0};
-            if (cb + k < niter && ro + 16 > 21) x[k] = ld16(p + ro);
-        }
+        const bool last_chunk = cb + kRowsPerChunk >= niter;
 #pragma unroll
         for (int k = 0; k < kRowsPerChunk; k++) {
             if (cb + k < niter) {
-                if (walk) reinterpret_cast<u32x4*>(stg)[k * 64 + l] = x[k];
-                const int64_t ro = g0 + ((cb + k) << 10) + 16 * (int64_t)l;
-                u32x4 y = x[k];
-                if (g0 + ((cb + k) << 10) < kHeaderSize) {
-                    // header image merge for bytes < 61 (row 0 and, when the
-                    // grid origin is below -963, row 1)
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const int64_t o4 = ro + 4 * q;
-                        const uint32_t im = img_dword(v_img, o4);
-                        uint32_t keep;  // raw bytes at offsets >= 61
-                        if (o4 >= kHeaderSize)
-                            keep = 0xffffffffu;
-                        else if (o4 + 4 <= kHeaderSize)
-                            keep = 0;
-                        else
-                            keep = 0xffffffffu << (8 * (uint32_t)(kHeaderSize - o4));
-                        const uint32_t raw = q == 0 ? y.x : q == 1 ? y.y : q == 2 ? y.z : y.w;
-                        const uint32_t v = (raw & keep) | (o4 >= kHeaderSize ? 0u : im);
-                        if (q == 0) y.x = v;
-                        if (q == 1) y.y = v;
-                        if (q == 2) y.z = v;
-                        if (q == 3) y.w = v;
-                    }
-                }
+                u32x4 y = pf.x[k];
+                if (k < 2 && cb == 0) y = merge_header(y, gm.g0 + ((int64_t)k << 10), v_img, l);
+                if (cb + k == niter - 1 && gm.pad) y = mask_pad(y, gm.pad, l);
                 y.x ^= c;
-                c = crc_block(sV, y);
+                c = crc_block(sN, y);
             }
-        }
-        if (walk && !whole) {
-            // too large to stage whole: exact walk chunk by chunk
-            wave_lds_sync();
-            const int64_t cbase = g0 + (cb << 10);
-            int64_t hi = cbase + ((int64_t)kRowsPerChunk << 10);
-            if (hi > n) hi = n;
-            walker_run(w, stg, cbase, hi, em);
-            wave_lds_sync();
+            // the row's registers now take row k of the next chunk, or of
+            // the next batch after the last chunk
+            // (one load either way: scalar selects of base and geometry)
+            const Geom lg = last_chunk ? ngm : gm;
+            const uint8_t* lp = last_chunk ? data + (has_next ? nd.offset : 0) : p;
+            pf.x[k] = load_row(batch_rsrc(lp), lg, last_chunk ? k : cb + kRowsPerChunk + k, l);
         }
     }
+    pf.gm = ngm;
+    STAMP(1);
+#ifndef RPGPU_DIAG_NO_COMBINE
     c = combine64(sT + kOffW, c);
+    if (gm.pad) c = apply8(sT + kOffP + gm.pad * 128, c);
+#endif
     r.crc = ~rdl(c, 0);
+#if defined(RPGPU_DIAG_NO_COMBINE) || defined(RPGPU_DIAG_NO_LOOKUP)  // keep verdicts OK
+    r.crc = r.crc_expected;
+#endif
+    STAMP(2);
 
     // ---- verdict precedence (kafka_batch_adapter.cc:169-193)
+    const uint8_t codec = (uint8_t)(r.h.attrs & 7);
     if (r.crc != r.crc_expected) {
         r.verdict = RPGPU_V_CRC_MISMATCH;
     } else if (body_trunc) {
         r.verdict = RPGPU_V_BODY_TRUNC_THROW;
     } else if (codec > 4) {
         r.verdict = RPGPU_V_BAD_CODEC_THROW;
-    } else if (walk) {
-        int32_t verdict;
-        uint32_t cnt;
-        if (whole) {
-            wave_lds_sync();
-            if (!fast_walk(stg, g0, n, r.h.record_count, cap, em, &verdict, &cnt))
-                slow_walk_whole(stg, g0, n, r.h.record_count, cap, em, &verdict, &cnt);
-        } else {
-            cnt = w.cnt < cap ? w.cnt : cap;
-            const uint32_t rem = cnt & 63u;
-            if (em.index && rem) flush_entries(w, em, rem, cnt - rem);
-            verdict = w.verdict;
+    } else if (codec == 0 && (d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX))) {
+        // walked with the rest of the group; the walk patches verdict and
+        // index_count
+        if (l == j) {
+            J.body = d.offset + kHeaderSize;
+            J.base_offset = r.h.base_offset;
+            J.first_ts = r.h.first_ts;
+            J.n = (uint32_t)(n - kHeaderSize);
+            J.rc = r.h.record_count;
+            J.first = index_first;
+            J.cap = cap;
+            J.b = b;
+            J.flags = kJobLive | ((d.ops & RPGPU_OP_INDEX) ? kJobIndex : 0u);
         }
-        r.verdict = verdict;
-        if (em.index) r.index_count = cnt;
     }
-    write_result(res, r);
+    write_result(res + b, r);
+    STAMP(3);
 }
 
-// One wave per batch, grid-stride.  index_first[i] = local exclusive prefix,
-// block_base[i / kScanBlock] = prefix of earlier scan blocks.
+// One wave per batch, grid-stride; every 64 batches of a wave are walked
+// together.  index_first[i] = local exclusive prefix, block_base[i /
+// kScanBlock] = prefix of earlier scan blocks.
 __global__ __launch_bounds__(kValidateThreads) void validate_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
     rpgpu_batch_result* __restrict__ res, rpgpu_record_index* __restrict__ index,
     const uint32_t* __restrict__ local_first, const uint32_t* __restrict__ caps,
     const uint64_t* __restrict__ block_base, uint64_t index_cap, const uint32_t* __restrict__ tables) {
     __shared__ __attribute__((aligned(16))) uint32_t sT[kTableWords];
-    __shared__ __attribute__((aligned(16))) uint32_t sStage[kWavesPerBlock * kStageWords];
     load_tables(sT, tables);
     const uint32_t wave = threadIdx.x >> 6;
-    uint32_t* stg = sStage + wave * kStageWords;
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + wave);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
-    for (uint32_t b = gw; b < n; b += nw) {
-        const rpgpu_batch_desc d = descs[b];
-        const uint64_t first = block_base[b / kScanBlock] + local_first[b];
-        // never write past the caller's index buffer (rpgpu_validate_device)
-        uint64_t cap = caps[b];
-        if (first >= index_cap) cap = 0;
-        else if (first + cap > index_cap) cap = index_cap - first;
-        process_batch(sT, stg, d, data, res + b, index, (uint32_t)first, (uint32_t)cap);
+#ifdef RPGPU_DIAG_STAMPS
+    Stamps sp{};
+    sp.prev = __builtin_amdgcn_s_memtime();
+#endif
+    Prefetch pf;
+    pf.gm = Geom{0, 0, 0};
+    if (gw < n) {
+        const rpgpu_batch_desc d0 = sload_desc(descs + gw);
+        const uint8_t* p0 = data + d0.offset;
+        const __amdgpu_buffer_rsrc_t rs0 = batch_rsrc(p0);
+        pf.hv = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs0, (int32_t)(4 * (lane_id() & 15)), 0, 0);
+        pf.gm = desc_geometry(d0, data);
+        load_rows(pf.x, rs0, pf.gm, 0, lane_id());
     }
+    for (uint32_t g = gw; g < n; g += kGroup * nw) {
+        WalkJob J;
+        J.flags = 0;
+        for (uint32_t j = 0; j < (uint32_t)kGroup; j++) {
+            const uint32_t b = g + j * nw;
+            if (b >= n) break;
+            const rpgpu_batch_desc d = sload_desc(descs + b);
+            const bool has_next = b + nw < n;
+            rpgpu_batch_desc nd{};
+            if (has_next) nd = sload_desc(descs + b + nw);
+            const uint64_t first = sload(block_base + b / kScanBlock) + sload(local_first + b);
+            // never write past the caller's index buffer (rpgpu_validate_device)
+            uint64_t cap = sload(caps + b);
+            if (first >= index_cap) cap = 0;
+            else if (first + cap > index_cap) cap = index_cap - first;
+            process_batch(sT, d, b, data, res, (uint32_t)first, (uint32_t)cap, pf, nd, has_next, J,
+                          j DIAG_PASS);
+        }
+        STAMP(5);
+        walk_lanes(data, J, index, res);
+        // the walk's loads are data-dependent in number: drain them here so
+        // that the next batch waits for its header window with a counted
+        // vmcnt, not for every row in flight
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        STAMP(4);
+    }
+#ifdef RPGPU_DIAG_STAMPS
+    if (lane_id() == 0)
+        for (int i = 0; i < 6; i++) atomicAdd(&g_stamps[i], (unsigned long long)sp.st[i]);
+#endif
 }
 
 // ------------------------------------------------------- index-cap prepass
@@ -470,7 +601,7 @@ __global__ __launch_bounds__(kValidateThreads) void crc_ranges_kernel(
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + wave);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
-    const uint32_t* sV = sT + kOffV;
+    const uint32_t* sV = sT + kOffN;
     for (uint32_t i = gw; i < n; i += nw) {
         const uint8_t* base = data + offs[i];
         const int64_t len = lens[i];
@@ -589,3 +720,12 @@ size_t validate_scratch_bytes(uint32_t n) {
 }
 
 }  // namespace rpgpu
+
+#ifdef RPGPU_DIAG_STAMPS
+// diagnostics build: read and clear the per-phase cycle sums
+extern "C" int rpgpu_diag_stamps(unsigned long long* out) {
+    unsigned long long z[8] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rpgpu::g_stamps), sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(rpgpu::g_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -5,11 +5,14 @@
 // implements for crc::crc32c, hashing/crc32c.h:21-43):
 //   S_k   = advance the state over k zero bytes (k may be negative: the map is
 //           invertible because the polynomial has a non-zero constant term);
-//   V[j]  = S_{j+1008} o T0 for j = 0..15  (slice-by-16 with the 1008-byte
-//           gap between one lane's consecutive blocks folded in);
+//   N[2i+h] = nibble h (0 low, 1 high) of byte i of a 16-byte block, followed
+//           by the block's remaining 15-i bytes and the 1008-byte gap to the
+//           lane's next block: S_{15-i+1008} o T0 restricted to that nibble;
 //   W[s]  = S_{-16*2^s} split into 8 nibble tables (butterfly combine);
 //   H     = S_{-960} as 8 nibble tables (header-CRC window correction);
-//   T0    = the plain byte table.
+//   T0    = the plain byte table;
+//   P[p]  = S_{-p}, p = 0..15, as nibble tables (drops the zero pad that
+//           extends a batch's CRC region to a 16-byte aligned end).
 #include <stdint.h>
 #include <string.h>
 
@@ -55,13 +58,17 @@ void build_tables(uint32_t* out) {
         for (int k = 0; k < 8; k++) c = bit_fwd(c);
         t0[b] = c;
     }
-    for (int j = 0; j < 16; j++) {
+    for (int i = 0; i < 16; i++) {
         uint32_t basis[32];
-        shift_basis(j + 1008, basis);
-        for (uint32_t b = 0; b < 256; b++) out[kOffV + j * 256 + b] = apply_basis(basis, t0[b]);
+        shift_basis(15 - i + 1008, basis);
+        for (uint32_t v = 0; v < 16; v++) {
+            out[kOffN + (2 * i) * 16 + v] = apply_basis(basis, t0[v]);
+            out[kOffN + (2 * i + 1) * 16 + v] = apply_basis(basis, t0[v << 4]);
+        }
     }
     for (int s = 0; s < 6; s++) nibble_tables(-16ll * (1ll << s), out + kOffW + s * 128);
     nibble_tables(-960, out + kOffH);
+    for (int p = 0; p < 16; p++) nibble_tables(-p, out + kOffP + p * 128);
 }
 
 }  // namespace rpgpu

@@ -1,20 +1,21 @@
-// rpgpu_walk.h — record field walk over a batch staged in LDS.
+// rpgpu_walk.h — record field walk, one lane per batch.
 //
 // Semantics: model/record.h:668-691 (for_each_record) over
 // model/record_utils.cc:93-176 (parse_one_record_copy_from_buffer), with the
 // iobuf parser bounds of bytes/iobuf_parser.h:48-52,100 and
-// bytes/iobuf.cc:136-160 (short copies are silent, lengths truncate to int).
+// bytes/iobuf.cc:136-160 (short copies are silent, lengths truncate to int),
+// as restated by oracle/batch.c walk_records.
 //
-// Two implementations with identical results:
-//   fast_walk    — a scalar chain over each record's `length` varint finds
-//                  the record starts, then one lane per record walks that
-//                  record's fields in VALU.  Valid only if every record's field
-//                  walk ends exactly where the chain put the next record; on
-//                  any anomaly (mismatch, end of body inside a record, varints
-//                  longer than 8 bytes, negative header count, ...) it gives up.
-//   walker_run   — the exact resumable state machine (wave-uniform scalar
-//                  code), used when fast_walk gives up and for batches too large
-//                  to stage whole (walked chunk by chunk).
+// The validate kernel checksums a group of up to 64 batches one after the
+// other (all 64 lanes on one batch), registering each batch that needs a
+// walk as a WalkJob in lane j of the group.  walk_lanes then walks all of
+// them at once, lane j over batch j.  The walk is a chain of dependent
+// reads (every field's position depends on the previous field's value), so
+// one batch per lane turns one wave's latency into 64 batches' progress.
+// Each lane reads its batch through a 32-byte register window reloaded at
+// the cursor when a field would run past it: for records with short keys,
+// one reload per record (at the header count, which the next record's
+// leading fields follow).
 #ifndef RPGPU_WALK_H
 #define RPGPU_WALK_H
 
@@ -22,326 +23,200 @@
 
 namespace rpgpu {
 
-enum WState : int32_t { WS_LEN = 0, WS_ATTR, WS_TS, WS_OFF, WS_KLEN, WS_VLEN, WS_HCOUNT, WS_HK, WS_HV, WS_DONE };
-
-struct Walker {
-    int64_t pos, n;  // batch-relative
-    int64_t vacc;
-    int32_t vshift;
-    int32_t state, verdict;
-    int32_t rec, rc;
-    int64_t h, hcount;
-    int64_t ts_delta, off_delta, klen, vlen;
-    int64_t key_off, val_off;
-    uint32_t cnt, cap;
-    // record-index staging for the serial walker: lane (cnt & 63) holds entry cnt
-    uint32_t e0, e1, e2, e3, e4, e5, e6, e7;
-};
-
-struct EmitCtx {
-    rpgpu_record_index* idx;  // already offset to this batch's first entry
+struct WalkJob {
+    uint64_t body;  // arena offset of the records (batch offset + 61)
     int64_t base_offset, first_ts;
-    bool index;
+    uint32_t n;      // body length in bytes
+    int32_t rc;      // header record_count
+    uint32_t first;  // index slot of the batch's first entry
+    uint32_t cap;    // index slots reserved for the batch
+    uint32_t b;      // batch number (result slot)
+    uint32_t flags;  // kJobLive | kJobIndex
+};
+constexpr uint32_t kJobLive = 1, kJobIndex = 2;
+
+// 32 bytes of the body starting at body offset `pos`.  Named scalars, not an
+// array: a select over array elements is folded back into a dynamically
+// indexed load, which would put the window in scratch memory.
+struct Window {
+    uint32_t w0, w1, w2, w3, w4, w5, w6, w7;
+    int64_t pos;
 };
 
-__device__ __forceinline__ void flush_entries(Walker& w, const EmitCtx& em, uint32_t count, uint32_t base) {
-    const uint32_t l = lane_id();
-    if (l < count) {
-        u32x4 a = {w.e0, w.e1, w.e2, w.e3};
-        u32x4 b = {w.e4, w.e5, w.e6, w.e7};
-        u32x4* dst = reinterpret_cast<u32x4*>(em.idx + base + l);
-        dst[0] = a;
-        dst[1] = b;
+__device__ __forceinline__ void window_load(Window& W, const uint8_t* body, int64_t pos) {
+    // RPGPU_ARENA_TAIL_PAD keeps the 32 bytes past any batch end readable
+    const u32x4 a = ld16(body + pos), b = ld16(body + pos + 16);
+    W.w0 = a.x, W.w1 = a.y, W.w2 = a.z, W.w3 = a.w;
+    W.w4 = b.x, W.w5 = b.y, W.w6 = b.z, W.w7 = b.w;
+    W.pos = pos;
+}
+
+// 12 bytes of the window from byte o (0 <= o < 32; zero past the window):
+// a three-stage select on the dword index, then a byte align.
+__device__ __forceinline__ void window_get(const Window& W, uint32_t o, uint32_t& d0, uint32_t& d1,
+                                           uint32_t& d2) {
+    const uint32_t q = o >> 2;
+    const bool s4 = q & 4, s2 = q & 2, s1 = q & 1;
+    const uint32_t u0 = s4 ? W.w4 : W.w0, u1 = s4 ? W.w5 : W.w1, u2 = s4 ? W.w6 : W.w2;
+    const uint32_t u3 = s4 ? W.w7 : W.w3, u4 = s4 ? 0u : W.w4, u5 = s4 ? 0u : W.w5, u6 = s4 ? 0u : W.w6;
+    const uint32_t v0 = s2 ? u2 : u0, v1 = s2 ? u3 : u1, v2 = s2 ? u4 : u2, v3 = s2 ? u5 : u3;
+    const uint32_t v4 = s2 ? u6 : u4;
+    const uint32_t t0 = s1 ? v1 : v0, t1 = s1 ? v2 : v1, t2 = s1 ? v3 : v2, t3 = s1 ? v4 : v3;
+    const uint32_t s = o & 3u;
+    d0 = __builtin_amdgcn_alignbyte(t1, t0, s);
+    d1 = __builtin_amdgcn_alignbyte(t2, t1, s);
+    d2 = __builtin_amdgcn_alignbyte(t3, t2, s);
+}
+
+// read_varlong (utils/vint.h:154-161 over the parser of bytes/iobuf_parser.h):
+// at most 10 bytes (the decoder stops once the shift passes 63), and at the
+// end of input a partial value of the bytes that were there.  Returns the
+// zigzag-decoded value and advances pos by the bytes consumed.
+__device__ __forceinline__ int64_t read_varlong(Window& W, const uint8_t* body, int64_t n, int64_t& pos) {
+    const int64_t avail = n - pos;
+    const uint32_t lim = avail <= 0 ? 0u : (avail < 10 ? (uint32_t)avail : 10u);
+    int64_t o = pos - W.pos;
+    uint32_t wa = o >= 32 ? 0u : 32u - (uint32_t)o;  // window bytes at the cursor
+    uint32_t d0, d1, d2;
+    window_get(W, (uint32_t)o, d0, d1, d2);
+    // first byte without the continuation bit among the window bytes
+    uint64_t x = ((uint64_t)d1 << 32) | d0;
+    uint64_t t8 = ~x & 0x8080808080808080ull;
+    uint32_t t2 = ~d2 & 0x8080u;
+    if (wa < 8) t8 &= (1ull << (8 * wa)) - 1;
+    if (wa < 10) t2 &= wa <= 8 ? 0u : 0x80u;
+    uint32_t term = t8 ? ((uint32_t)__builtin_ctzll(t8) >> 3) : (t2 ? 8u + ((uint32_t)__builtin_ctz(t2) >> 3) : 10u);
+    if (term >= lim ? lim > wa : false) {
+        // the bytes this read consumes run past the window: reload at the cursor
+        window_load(W, body, pos);
+        window_get(W, 0, d0, d1, d2);
+        x = ((uint64_t)d1 << 32) | d0;
+        t8 = ~x & 0x8080808080808080ull;
+        t2 = ~d2 & 0x8080u;
+        term = t8 ? ((uint32_t)__builtin_ctzll(t8) >> 3) : (t2 ? 8u + ((uint32_t)__builtin_ctz(t2) >> 3) : 10u);
     }
+    const uint32_t nb = term < lim ? term + 1 : lim;
+    uint64_t y = x & 0x7f7f7f7f7f7f7f7full;
+    if (nb < 8) y &= (1ull << (8 * nb)) - 1;
+    y = (y & 0x007f007f007f007full) | ((y & 0x7f007f007f007f00ull) >> 1);
+    y = (y & 0x00003fff00003fffull) | ((y & 0x3fff00003fff0000ull) >> 2);
+    y = (y & 0x000000000fffffffull) | ((y & 0x0fffffff00000000ull) >> 4);
+    if (nb > 8) y |= (uint64_t)(d2 & 0x7fu) << 56;
+    if (nb > 9) y |= (uint64_t)((d2 >> 8) & 1u) << 63;
+    pos += nb;
+    return (int64_t)((y >> 1) ^ (~(y & 1) + 1));
+}
+
+// iobuf_parser::copy -> iobuf_copy (bytes/iobuf.cc:136-160): the length is
+// truncated to int; copies beyond kCopyLimit or negative ones depend on the
+// reference broker's memory and are reported as REC_UNDEFINED.
+__device__ __forceinline__ bool parser_copy(int64_t n, int64_t& pos, int64_t len) {
+    const int32_t l32 = (int32_t)(uint32_t)(uint64_t)len;
+    if (l32 < 0 || (uint32_t)l32 > kCopyLimit) return false;
+    const int64_t left = n - pos;
+    pos += (int64_t)l32 < left ? (int64_t)l32 : left;
+    return true;
 }
 
 __device__ __forceinline__ void store_entry(rpgpu_record_index* e, int64_t off, int64_t ts, uint32_t koff,
                                             int32_t klen, uint32_t voff, int32_t vlen) {
-    u32x4 a = {(uint32_t)(uint64_t)off, (uint32_t)((uint64_t)off >> 32), (uint32_t)(uint64_t)ts,
-               (uint32_t)((uint64_t)ts >> 32)};
-    u32x4 b = {koff, (uint32_t)klen, voff, (uint32_t)vlen};
+    const u32x4 a = {(uint32_t)(uint64_t)off, (uint32_t)((uint64_t)off >> 32), (uint32_t)(uint64_t)ts,
+                     (uint32_t)((uint64_t)ts >> 32)};
+    const u32x4 b = {koff, (uint32_t)klen, voff, (uint32_t)vlen};
     u32x4* dst = reinterpret_cast<u32x4*>(e);
     dst[0] = a;
     dst[1] = b;
 }
 
-__device__ __forceinline__ void finish_record(Walker& w, const EmitCtx& em) {
-    if (em.index && w.cnt < w.cap) {
-        const uint32_t slot = w.cnt & 63u;
-        const int64_t off = (int64_t)((uint64_t)em.base_offset + (uint64_t)(int64_t)(int32_t)w.off_delta);
-        const int64_t ts = (int64_t)((uint64_t)em.first_ts + (uint64_t)w.ts_delta);
-        const bool me = lane_id() == slot;
-        w.e0 = me ? (uint32_t)off : w.e0;
-        w.e1 = me ? (uint32_t)((uint64_t)off >> 32) : w.e1;
-        w.e2 = me ? (uint32_t)ts : w.e2;
-        w.e3 = me ? (uint32_t)((uint64_t)ts >> 32) : w.e3;
-        w.e4 = me ? (uint32_t)w.key_off : w.e4;
-        w.e5 = me ? (uint32_t)(int32_t)w.klen : w.e5;
-        w.e6 = me ? (uint32_t)w.val_off : w.e6;
-        w.e7 = me ? (uint32_t)(int32_t)w.vlen : w.e7;
-        if (slot == 63u) flush_entries(w, em, 64u, w.cnt - 63u);
-    }
-    w.cnt++;
-    w.rec++;
-    if (w.rec < w.rc) {
-        w.state = WS_LEN;
-    } else {
-        w.state = WS_DONE;
-        w.verdict = (w.pos < w.n) ? RPGPU_V_REC_TRAILING : RPGPU_V_OK;
-    }
-}
-
-// iobuf_copy (bytes/iobuf.cc:136-160): int truncation, silent short copy.
-__device__ __forceinline__ bool walker_copy(Walker& w, int64_t len) {
-    const int32_t l32 = (int32_t)(uint32_t)(uint64_t)len;
-    if (l32 < 0 || (uint32_t)l32 > kCopyLimit) {
-        w.verdict = RPGPU_V_REC_UNDEFINED;
-        w.state = WS_DONE;
-        return false;
-    }
-    const int64_t room = w.n - w.pos;
-    w.pos += ((int64_t)l32 < room) ? (int64_t)l32 : room;
-    return true;
-}
-
-__device__ __forceinline__ void walker_init(Walker& w, int64_t n, int32_t rc, uint32_t cap, bool active) {
-    w.pos = kHeaderSize;
-    w.n = n;
-    w.vacc = 0;
-    w.vshift = 0;
-    w.rec = 0;
-    w.rc = rc;
-    w.cnt = 0;
-    w.cap = cap;
-    w.h = 0;
-    w.hcount = 0;
-    w.e0 = w.e1 = w.e2 = w.e3 = w.e4 = w.e5 = w.e6 = w.e7 = 0;
-    w.ts_delta = w.off_delta = w.klen = w.vlen = w.key_off = w.val_off = 0;
-    if (!active) {
-        w.state = WS_DONE;
-        w.verdict = RPGPU_V_OK;
-    } else if (rc <= 0) {
-        w.state = WS_DONE;
-        w.verdict = (w.pos < n) ? RPGPU_V_REC_TRAILING : RPGPU_V_OK;
-    } else {
-        w.state = WS_LEN;
-        w.verdict = RPGPU_V_OK;
-    }
-}
-
-// Exact serial walk through the bytes staged in LDS: batch offsets
-// [cbase, hi) live at stg[0 .. hi - cbase).  Returns when it needs a byte
-// at or beyond `hi` (< n) or when the walk is done.
-__device__ __noinline__ void walker_run(Walker& w, const uint32_t* stg, int64_t cbase, int64_t hi,
-                                        EmitCtx em) {
-    uint32_t cached_dw = 0xffffffffu, cached = 0;
-    while (w.state != WS_DONE) {
-        if (w.state == WS_ATTR) {
-            // consume_type<int8_t> (record_utils.cc:158): throws at end
-            if (w.pos >= w.n) {
-                w.verdict = RPGPU_V_REC_ATTR_EOF;
-                w.state = WS_DONE;
-                break;
-            }
-            w.pos += 1;
-            w.state = WS_TS;
-            continue;
-        }
-        if (w.state == WS_HK && w.pos >= w.n) {
-            // remaining header iterations read (0,0) and copy nothing
-            finish_record(w, em);
-            continue;
-        }
-        // varint decode (utils/vint.h:35-64, limit 63)
-        bool complete = false;
-        while (true) {
-            if (w.vshift > 63 || w.pos >= w.n) {
-                complete = true;
-                break;
-            }
-            if (w.pos >= hi) break;  // byte is in the next chunk
-            const uint32_t rel = (uint32_t)(w.pos - cbase);
-            const uint32_t dw = rel >> 2;
-            if (dw != cached_dw) {
-                cached = __builtin_amdgcn_readfirstlane(stg[dw]);
-                cached_dw = dw;
-            }
-            const uint64_t b = (cached >> ((rel & 3u) * 8u)) & 255u;
-            w.pos += 1;
-            w.vacc |= (int64_t)((b & 127u) << (uint32_t)w.vshift);
-            if (!(b & 128u)) {
-                complete = true;
-                break;
-            }
-            w.vshift += 7;
-        }
-        if (!complete) return;
-        const uint64_t u = (uint64_t)w.vacc;
-        const int64_t v = (int64_t)((u >> 1) ^ (~(u & 1) + 1));
-        w.vacc = 0;
-        w.vshift = 0;
-        switch (w.state) {
-        case WS_LEN: w.state = WS_ATTR; break;
-        case WS_TS:
-            w.ts_delta = v;
-            w.state = WS_OFF;
-            break;
-        case WS_OFF:
-            w.off_delta = v;
-            w.state = WS_KLEN;
-            break;
-        case WS_KLEN:
-            w.klen = v;
-            w.key_off = w.pos;
-            if (v > 0 && !walker_copy(w, v)) break;
-            w.state = WS_VLEN;
-            break;
-        case WS_VLEN:
-            w.vlen = v;
-            w.val_off = w.pos;
-            if (v > 0 && !walker_copy(w, v)) break;
-            w.state = WS_HCOUNT;
-            break;
-        case WS_HCOUNT:
-            if (v < 0) {  // headers.reserve(negative) -> std::length_error
-                w.verdict = RPGPU_V_REC_HCOUNT_NEG;
-                w.state = WS_DONE;
-                break;
-            }
-            if (v > kHcountLimit) {
-                w.verdict = RPGPU_V_REC_UNDEFINED;
-                w.state = WS_DONE;
-                break;
-            }
-            w.hcount = v;
-            w.h = 0;
-            if (v == 0)
-                finish_record(w, em);
-            else
-                w.state = WS_HK;
-            break;
-        case WS_HK:
-            if (v > 0 && !walker_copy(w, v)) break;
-            w.state = WS_HV;
-            break;
-        case WS_HV:
-            if (v > 0 && !walker_copy(w, v)) break;
-            w.h += 1;
-            if (w.h < w.hcount)
-                w.state = WS_HK;
-            else
-                finish_record(w, em);
-            break;
-        default: break;
-        }
-    }
-}
-
-// Exact walk of a batch staged whole, from scratch (fast_walk's fallback).
-__device__ __noinline__ void slow_walk_whole(const uint32_t* stg, int64_t g0, int64_t n, int32_t rc,
-                                             uint32_t cap, EmitCtx em, int32_t* verdict,
-                                             uint32_t* count) {
-    Walker w;
-    walker_init(w, n, rc, cap, true);
-    walker_run(w, stg, g0, n, em);
-    const uint32_t cnt = w.cnt < cap ? w.cnt : cap;
-    const uint32_t rem = cnt & 63u;
-    if (em.index && rem) flush_entries(w, em, rem, cnt - rem);
-    *verdict = w.verdict;
-    *count = cnt;
-}
-
-// Fast path for a batch staged whole (stg[rel] = batch byte g0 + rel).
-// Returns false (and writes nothing the caller relies on) on any anomaly.
-__device__ __forceinline__ bool fast_walk(const uint32_t* stg, int64_t g0, int64_t n, int32_t rc,
-                                          uint32_t cap, const EmitCtx& em, int32_t* verdict,
-                                          uint32_t* count) {
-    const uint32_t l = lane_id();
-    int64_t s = kHeaderSize;
-    int32_t j = 0;
+// Walks lane j's batch; writes its verdict and index_count into its result
+// (the rest of the result was written when the batch was checksummed).
+__device__ __forceinline__ void walk_lanes(const uint8_t* __restrict__ data, WalkJob J,
+                                        rpgpu_record_index* __restrict__ index,
+                                        rpgpu_batch_result* __restrict__ res) {
+    bool live = (J.flags & kJobLive) != 0;
+    const uint8_t* body = data + J.body;
+    const int64_t n = J.n;
+    int64_t pos = 0;
     uint32_t cnt = 0;
-    if (rc <= 0) {
-        *verdict = (s < n) ? RPGPU_V_REC_TRAILING : RPGPU_V_OK;
-        *count = 0;
-        return true;
-    }
-    while (j < rc) {
-        // chain: record starts from the length varints, up to 64 at a time
-        int64_t st = 0;
-        uint32_t g = 0;
-        while (g < 64 && j < rc && s < n) {
-            const Var f = var8(stg8(stg, (uint32_t)(s - g0)), n - s);
-            if (!f.ok || f.v < 0 || f.v > n - s - (int64_t)f.nb) return false;
-            st = (l == g) ? s : st;
-            s += (int64_t)f.nb + f.v;
-            g++;
-            j++;
+    int32_t i = 0;
+    int32_t verdict = RPGPU_V_OK;
+    Window W;
+    W.pos = 0;
+    if (live) window_load(W, body, 0);
+    rpgpu_record_index* idx = index + J.first;
+    while (wave_any(live)) {
+        if (!live) continue;
+        if (i >= J.rc) {  // record.h:686-690
+            verdict = pos < n ? RPGPU_V_REC_TRAILING : RPGPU_V_OK;
+            live = false;
+            continue;
         }
-        if (g == 0) break;
-        // one lane per record: the reference's field walk
-        const bool act = l < g;
+        (void)read_varlong(W, body, n, pos);  // record size: not used by the parse
+        if (pos >= n) {                       // consume_type<int8_t> throws
+            verdict = RPGPU_V_REC_ATTR_EOF;
+            live = false;
+            continue;
+        }
+        pos += 1;  // attributes
+        const int64_t ts_delta = read_varlong(W, body, n, pos);
+        const int64_t off_delta = read_varlong(W, body, n, pos);
+        const int64_t klen = read_varlong(W, body, n, pos);
+        const int64_t key_off = pos;
+        if (klen > 0 && !parser_copy(n, pos, klen)) {
+            verdict = RPGPU_V_REC_UNDEFINED;
+            live = false;
+            continue;
+        }
+        const int64_t vlen = read_varlong(W, body, n, pos);
+        const int64_t val_off = pos;
+        if (vlen > 0 && !parser_copy(n, pos, vlen)) {
+            verdict = RPGPU_V_REC_UNDEFINED;
+            live = false;
+            continue;
+        }
+        // parse_record_headers (record_utils.cc:93-114)
+        const int64_t hcount = read_varlong(W, body, n, pos);
+        if (hcount < 0) {  // reserve(size_t(negative)) -> length_error
+            verdict = RPGPU_V_REC_HCOUNT_NEG;
+            live = false;
+            continue;
+        }
+        if (hcount > kHcountLimit) {
+            verdict = RPGPU_V_REC_UNDEFINED;
+            live = false;
+            continue;
+        }
         bool bad = false;
-        int64_t p = st, end = 0, ts = 0, off = 0, klen = 0, vlen = 0, koff = 0, voff = 0, hc = 0;
-        auto dec = [&](int64_t& q) -> int64_t {
-            const int64_t rr = q - g0;
-            const uint32_t r = (rr < 0 || rr > (int64_t)kStageBytes) ? (uint32_t)kStageBytes : (uint32_t)rr;
-            const Var f = var8(stg8(stg, r), n - q);
-            bad |= !f.ok;
-            q += f.nb;
-            return f.v;
-        };
-        if (act) {
-            const int64_t len = dec(p);
-            end = p + len;
-            if (p >= n) bad = true;  // record attributes byte
-            p += 1;
-            ts = dec(p);
-            off = dec(p);
-            klen = dec(p);
-            koff = p;
-            if (klen > 0) {
-                if (klen > n - p) bad = true;
-                else p += klen;
+        for (int64_t h = 0; h < hcount; h++) {
+            if (pos >= n) break;  // every further header is a no-op at end of input
+            const int64_t hk = read_varlong(W, body, n, pos);
+            if (hk > 0 && !parser_copy(n, pos, hk)) {
+                bad = true;
+                break;
             }
-            vlen = dec(p);
-            voff = p;
-            if (vlen > 0) {
-                if (vlen > n - p) bad = true;
-                else p += vlen;
-            }
-            hc = dec(p);
-            if (hc < 0 || hc > kHcountLimit) bad = true;
-        }
-        int64_t h = 0;
-        while (wave_any(act && !bad && h < hc)) {
-            if (act && !bad && h < hc) {
-                const int64_t hk = dec(p);
-                if (hk > 0) {
-                    if (hk > n - p) bad = true;
-                    else p += hk;
-                }
-                const int64_t hv = dec(p);
-                if (hv > 0) {
-                    if (hv > n - p) bad = true;
-                    else p += hv;
-                }
-                h++;
+            const int64_t hv = read_varlong(W, body, n, pos);
+            if (hv > 0 && !parser_copy(n, pos, hv)) {
+                bad = true;
+                break;
             }
         }
-        if (wave_any(act && (bad || p != end))) return false;
-        if (em.index && act && cnt + l < cap) {
-            store_entry(em.idx + cnt + l,
-                        (int64_t)((uint64_t)em.base_offset + (uint64_t)(int64_t)(int32_t)off),
-                        (int64_t)((uint64_t)em.first_ts + (uint64_t)ts), (uint32_t)koff, (int32_t)klen,
-                        (uint32_t)voff, (int32_t)vlen);
+        if (bad) {
+            verdict = RPGPU_V_REC_UNDEFINED;
+            live = false;
+            continue;
         }
-        cnt += g;
+        if ((J.flags & kJobIndex) && cnt < J.cap)
+            store_entry(idx + cnt, (int64_t)((uint64_t)J.base_offset + (uint64_t)(int64_t)(int32_t)off_delta),
+                        (int64_t)((uint64_t)J.first_ts + (uint64_t)ts_delta), (uint32_t)(key_off + kHeaderSize),
+                        (int32_t)klen, (uint32_t)(val_off + kHeaderSize), (int32_t)vlen);
+        cnt++;
+        i++;
     }
-    *count = cnt < cap ? cnt : cap;
-    // after record_count records: trailing bytes throw (record.h:686-690);
-    // running out first means the next record's attributes read throws
-    *verdict = (j == rc) ? ((s < n) ? RPGPU_V_REC_TRAILING : RPGPU_V_OK) : RPGPU_V_REC_ATTR_EOF;
-    return true;
+    if (J.flags & kJobLive) {
+        uint32_t* r = reinterpret_cast<uint32_t*>(res + J.b);
+        r[0] = (uint32_t)verdict;                                           // .verdict
+        r[15] = (J.flags & kJobIndex) ? (cnt < J.cap ? cnt : J.cap) : 0u;  // .index_count
+    }
 }
 
 }  // namespace rpgpu

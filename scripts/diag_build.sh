@@ -1,0 +1,10 @@
+# Diagnostics builds of librpgpu.so with parts of the validate kernel compiled
+# out (timing attribution only; results are not valid).  Output: build/diag/
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p build/diag
+for v in ${DIAG_VARIANTS:-NO_LOOKUP NO_COMBINE STAMPS}; do
+  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DRPGPU_DIAG_$v -Iinclude -Iredpanda_amd/csrc \
+    redpanda_amd/csrc/rpgpu_kernels.hip redpanda_amd/csrc/rpgpu_abi.cpp redpanda_amd/csrc/rpgpu_tables.cpp \
+    -o build/diag/librpgpu_$v.so
+done
