@@ -6,6 +6,7 @@ raises instead of falling back to anything on the CPU.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
 import numpy as np
@@ -111,7 +112,8 @@ def lib() -> C.CDLL:
     """The HIP engine (librpgpu.so).  Raises if it has not been built."""
     global _LIB
     if _LIB is None:
-        path = PKG / "librpgpu.so"
+        # RPGPU_DIAG_LIB: a diagnostics build (scripts/diag_build.sh), never the default
+        path = Path(os.environ.get("RPGPU_DIAG_LIB", PKG / "librpgpu.so"))
         if not path.exists():
             raise RuntimeError(f"{path} is missing: run __graft_entry__.build() "
                                "(the engine has no CPU fallback)")
