@@ -21,14 +21,14 @@ constexpr int kOffN = 0;                 // 32 x 16: block nibble tables, pre-sh
 constexpr int kOffW = kOffN + 32 * 16;   // 6 x 8 x 16: x^(-8*16*2^s), nibble tables
 constexpr int kOffH = kOffW + 6 * 128;   // 8 x 16: x^(-8*960), nibble tables
 constexpr int kOffT0 = kOffH + 128;      // 256: plain byte table (ranges shorter than 4 B)
-constexpr int kOffP = kOffT0 + 256;      // 16 x 8 x 16: x^(-8*p), p = 0..15 (row-grid pad)
-constexpr int kTableWords = kOffP + 16 * 128;
+constexpr int kRowsPerChunk = 8;        // 8 x 1 KiB rows in flight per wave
+constexpr int kOffU = kOffT0 + 256;      // kRowsPerChunk x 8 x 16: x^(-8*1024*m) (phantom rows)
+constexpr int kTableWords = kOffU + kRowsPerChunk * 128;
 static_assert(kTableWords % 4 == 0, "table blob is copied as 16-byte words");
 
 constexpr int kValidateThreads = 256;  // 4 waves per workgroup
 constexpr int kWavesPerBlock = kValidateThreads / 64;
 constexpr int kBlocksPerCU = 4;        // default grid: 16 waves per CU
-constexpr int kRowsPerChunk = 16;      // 16 x 1 KiB rows in flight per wave
 constexpr int kGroup = 64;             // batches per wave between record walks (one per lane)
 constexpr int kScanBlock = 1024;
 

@@ -5,21 +5,22 @@
 //
 // (1) CRC32C, all 64 lanes on one batch ("strided rows").  The Kafka CRC
 // covers batch bytes [21, n) (kafka_batch_adapter.cc:99-134).  The region is
-// extended to a 16-byte aligned END (the extension is zeroed and removed at
-// the end with the map x^(-8*pad), tables P) and cut into 16-byte blocks
-// counted from that end; 64 consecutive blocks form a 1 KiB "row", lane l of
-// row t owning block r = 64t + 63 - l, so every row is one aligned,
-// coalesced 1 KiB load (16 B per lane).  Each lane keeps its own CRC state
-// over the blocks it owns; they are 1008 bytes apart, so the tables are
-// pre-multiplied by x^(8*1008) and a lane advances with 32 nibble lookups per
-// 16 bytes (16-entry tables: no LDS bank conflicts).  A 6-step butterfly
-// folds the 64 lane states (tables W).  The CRC init is folded into the
-// first four bytes of the message and bytes before the region are zeroed.
-// Header bytes [21, 61) are taken from an "image" built from the parsed
-// header (big-endian, as crc_record_batch_header hashes them,
-// record_utils.cc:68-80), so one loop serves wire and on-disk batches.
-// The next batch's rows are loaded into the registers each row frees as it
-// is checksummed, so 16 KiB per wave stay in flight.
+// cut into 1 KiB rows aligned to its END (the last row ends at n, so nothing
+// past the batch is hashed and the tail needs no masking); row t is one
+// coalesced 1 KiB load, 16 B per lane, lane l owning block 64t + l.  Each
+// lane keeps its own CRC state over the blocks it owns; they are 1008 bytes
+// apart, so the tables are pre-multiplied by x^(8*1008) and a lane advances
+// with 32 nibble lookups per 16 bytes (16-entry tables: no LDS bank
+// conflicts).  Rows are processed in straight-line chunks of kRowsPerChunk;
+// the all-zero phantom rows that round a batch up to whole chunks shift
+// every lane by 1 KiB each and are undone at the end (tables U).  A 6-step
+// butterfly folds the 64 lane states (tables W).  Bytes [0, 61) of rows 0
+// and 1 are replaced by an "image" built from the parsed header: zeros
+// before 21, big-endian fields in [21, 61) as crc_record_batch_header
+// hashes them (record_utils.cc:68-80), the CRC init folded into [21, 25),
+// so one loop serves wire and on-disk batches.  The next chunk's (or next
+// batch's) rows are loaded into the registers each row frees as it is
+// checksummed, so 8 KiB per wave stay in flight.
 //
 // (2) Record walk (rpgpu_walk.h), one lane per batch of the group.
 #include "rpgpu_device.h"
@@ -120,19 +121,23 @@ __device__ __forceinline__ uint32_t header_crc_vec(const uint32_t* sT, const Img
     return ~rdl(c, 0);
 }
 
-// Row geometry of the CRC region [21, n) of a batch starting at absolute
-// address `at`: the end is extended by `pad` bytes to a 16-byte boundary;
-// niter 1 KiB rows end there, row k starts at batch offset g0 + 1024 k.
+// Row geometry of the CRC region [21, n) of a batch: 1 KiB rows aligned to
+// the region's END (row k covers batch bytes [g0 + 1024 k, +1024), the last
+// row ends exactly at n), so no byte past the batch is ever hashed.  Rows
+// are processed in chunks of kRowsPerChunk; the rows that round niter up to
+// whole chunks are "phantom" rows past the end that read as zeros and
+// advance every lane state by 1 KiB (undone with tables U).  Batches are
+// shorter than 2^31 bytes (Kafka's batch_length is an int32), so 32-bit
+// scalar arithmetic suffices (64-bit compares would run on the VALU).
 struct Geom {
-    int64_t niter, g0;
-    uint32_t pad;
+    int32_t niter, g0;
 };
-__device__ __forceinline__ Geom geometry(uint64_t at, int64_t n) {
-    const uint32_t pad = (uint32_t)(0 - (at + (uint64_t)n)) & 15u;
-    const int64_t ne = n + pad;
-    const int64_t nblocks = (ne - 21 + 15) >> 4;
-    const int64_t niter = (nblocks + 63) >> 6;
-    return Geom{niter, ne - (niter << 10), pad};
+__device__ __forceinline__ Geom geometry(int32_t n) {
+    const int32_t niter = (n - 21 + 1023) >> 10;
+    return Geom{niter, n - (niter << 10)};
+}
+__device__ __forceinline__ int32_t chunk_rows(int32_t niter) {
+    return (niter + kRowsPerChunk - 1) & ~(kRowsPerChunk - 1);
 }
 
 // One batch's first chunk of rows and its 64-byte header window, loaded
@@ -145,41 +150,41 @@ struct Prefetch {
 };
 
 // Rows are read through a buffer resource based at the batch start: lanes
-// whose block starts before the batch (negative offset, out of range as an
-// unsigned offset) and rows past the region (offset 2^31) read zeros
-// without touching memory.  The load is always issued, so the number of
-// loads per batch is fixed and the compiler waits for one row with a counted
-// vmcnt instead of draining every row in flight.  Batches are shorter than
-// 2^31 bytes (Kafka's batch_length is an int32; RPGPU_MAX_BATCH_BYTES).
+// whose 16 bytes start before the batch (negative offset, out of range as
+// an unsigned offset) and phantom rows (offset 2^31) read zeros without
+// touching memory.  The load is always issued, so the number of loads per
+// batch is fixed and the compiler waits for one row with a counted vmcnt
+// instead of draining every row in flight.
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t batch_rsrc(const uint8_t* p) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p), 0, 0x7ffffff0, 0x00020000);
 }
-__device__ __forceinline__ u32x4 load_row(__amdgpu_buffer_rsrc_t rs, const Geom& gm, int64_t row, uint32_t l) {
-    const int32_t rb = row < gm.niter ? (int32_t)(gm.g0 + (row << 10)) : (int32_t)0x80000000;
+__device__ __forceinline__ u32x4 load_row(__amdgpu_buffer_rsrc_t rs, const Geom& gm, int32_t row, uint32_t l) {
+    const int32_t rb = row < gm.niter ? gm.g0 + (row << 10) : (int32_t)0x80000000;
     const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, rb + (int32_t)(16 * l), 0, 0);
     return (u32x4){(uint32_t)v.x, (uint32_t)v.y, (uint32_t)v.z, (uint32_t)v.w};
 }
 
 __device__ __forceinline__ void load_rows(u32x4 (&x)[kRowsPerChunk], __amdgpu_buffer_rsrc_t rs, const Geom& gm,
-                                          int64_t cb, uint32_t l) {
+                                          int32_t cb, uint32_t l) {
 #pragma unroll
     for (int k = 0; k < kRowsPerChunk; k++) x[k] = load_row(rs, gm, cb + k, l);
 }
 
-__device__ __forceinline__ Geom desc_geometry(const rpgpu_batch_desc& d, const uint8_t* data) {
-    return d.length >= (uint32_t)kHeaderSize ? geometry((uint64_t)(data + d.offset), d.length) : Geom{0, 0, 0};
+__device__ __forceinline__ Geom desc_geometry(const rpgpu_batch_desc& d) {
+    return d.length >= (uint32_t)kHeaderSize ? geometry((int32_t)d.length) : Geom{0, 0};
 }
 
 // Row block at batch offset ro0 + 16*lane with bytes [0, 61) replaced by the
 // header image (zero below 21, big-endian fields in [21, 61), CRC init folded
-// into [21, 25)); rows starting at or after 61 pass through.
-__device__ __forceinline__ u32x4 merge_header(u32x4 y, int64_t ro0, uint32_t v_img, uint32_t l) {
+// into [21, 25)); rows starting at or after 61 pass through.  Whatever the
+// load returned for bytes before the batch start is masked away.
+__device__ __forceinline__ u32x4 merge_header(u32x4 y, int32_t ro0, uint32_t v_img, uint32_t l) {
     if (ro0 >= kHeaderSize) return y;
-    const int64_t ro = ro0 + 16 * (int64_t)l;
+    const int32_t ro = ro0 + 16 * (int32_t)l;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        const int64_t o4 = ro + 4 * q;
+        const int32_t o4 = ro + 4 * q;
         const uint32_t im = img_dword(v_img, o4);
         uint32_t keep;  // raw bytes at offsets >= 61
         if (o4 >= kHeaderSize)
@@ -194,22 +199,6 @@ __device__ __forceinline__ u32x4 merge_header(u32x4 y, int64_t ro0, uint32_t v_i
         if (q == 1) y.y = v;
         if (q == 2) y.z = v;
         if (q == 3) y.w = v;
-    }
-    return y;
-}
-
-// last block of the region (lane 63 of the last row): zero the pad bytes
-__device__ __forceinline__ u32x4 mask_pad(u32x4 y, uint32_t pad, uint32_t l) {
-    const uint32_t keep = 16u - pad;  // bytes of the block inside the region
-    uint32_t m[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-        m[q] = keep >= 4u * q + 4 ? 0xffffffffu : (keep <= 4u * q ? 0u : (1u << (8 * (keep - 4 * q))) - 1);
-    if (l == 63) {
-        y.x &= m[0];
-        y.y &= m[1];
-        y.z &= m[2];
-        y.w &= m[3];
     }
     return y;
 }
@@ -237,12 +226,12 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
     Img64 H;
 #pragma unroll
     for (int i = 0; i < 16; i++) H.w[i] = rdl(hv, i);
-    Geom ngm{0, 0, 0};
+    Geom ngm{0, 0};
     // always issued (lanes 16..63 repeat the window): a fixed load count
     // keeps the compiler's vmcnt bookkeeping exact
     const __amdgpu_buffer_rsrc_t nrs = batch_rsrc(data + (has_next ? nd.offset : 0));
     pf.hv = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(nrs, (int32_t)(4 * (l & 15)), 0, 0);
-    if (has_next) ngm = desc_geometry(nd, data);
+    if (has_next) ngm = desc_geometry(nd);
 
     Img64 D;  // little-endian disk header image (CRC'd bytes [4, 61))
     D.clear();
@@ -372,38 +361,40 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
     for (int i = 0; i < 16; i++) v_img = (l == (uint32_t)i) ? B.w[i] : v_img;
 
     // ---- rows over the CRC region [21, n)
-    const Geom gm = geometry((uint64_t)p, n);
-    const int64_t niter = gm.niter;
-    const bool pf_ok = pf.gm.niter == niter && pf.gm.g0 == gm.g0;  // prefetch geometry matches
+    const Geom gm = geometry((int32_t)n);
+    const int32_t nrows = chunk_rows(gm.niter);  // real + phantom rows
+    const bool pf_ok = pf.gm.niter == gm.niter && pf.gm.g0 == gm.g0;  // prefetch geometry matches
     const uint32_t* sN = sT + kOffN;
     const __amdgpu_buffer_rsrc_t rs = batch_rsrc(p);
+    const __amdgpu_buffer_rsrc_t nrs_rows = batch_rsrc(data + (has_next ? nd.offset : 0));
     uint32_t c = 0;
     STAMP(0);
     if (!pf_ok) load_rows(pf.x, rs, gm, 0, l);
-    for (int64_t cb = 0; cb < niter; cb += kRowsPerChunk) {
-        const bool last_chunk = cb + kRowsPerChunk >= niter;
+    // the header bytes lie in rows 0 and 1
+    pf.x[0] = merge_header(pf.x[0], gm.g0, v_img, l);
+    pf.x[1] = merge_header(pf.x[1], gm.g0 + 1024, v_img, l);
+    for (int32_t cb = 0; cb < nrows; cb += kRowsPerChunk) {
+        // each row's registers take row k of the next chunk once the row is
+        // checksummed, or row k of the next batch during the last chunk
+        const bool last_chunk = cb + kRowsPerChunk >= nrows;
+        const __amdgpu_buffer_rsrc_t lrs = last_chunk ? nrs_rows : rs;
+        const Geom lg = last_chunk ? ngm : gm;
+        const int32_t lrow = last_chunk ? 0 : cb + kRowsPerChunk;
+        // one straight-line block: the lookups of row k+1 that do not
+        // depend on the lane state overlap row k's
 #pragma unroll
         for (int k = 0; k < kRowsPerChunk; k++) {
-            if (cb + k < niter) {
-                u32x4 y = pf.x[k];
-                if (k < 2 && cb == 0) y = merge_header(y, gm.g0 + ((int64_t)k << 10), v_img, l);
-                if (cb + k == niter - 1 && gm.pad) y = mask_pad(y, gm.pad, l);
-                y.x ^= c;
-                c = crc_block(sN, y);
-            }
-            // the row's registers now take row k of the next chunk, or of
-            // the next batch after the last chunk
-            // (one load either way: scalar selects of base and geometry)
-            const Geom lg = last_chunk ? ngm : gm;
-            const uint8_t* lp = last_chunk ? data + (has_next ? nd.offset : 0) : p;
-            pf.x[k] = load_row(batch_rsrc(lp), lg, last_chunk ? k : cb + kRowsPerChunk + k, l);
+            u32x4 y = pf.x[k];
+            y.x ^= c;
+            c = crc_block(sN, y);
+            pf.x[k] = load_row(lrs, lg, lrow + k, l);
         }
     }
     pf.gm = ngm;
     STAMP(1);
 #ifndef RPGPU_DIAG_NO_COMBINE
     c = combine64(sT + kOffW, c);
-    if (gm.pad) c = apply8(sT + kOffP + gm.pad * 128, c);
+    if (nrows != gm.niter) c = apply8(sT + kOffU + (nrows - gm.niter) * 128, c);
 #endif
     r.crc = ~rdl(c, 0);
 #if defined(RPGPU_DIAG_NO_COMBINE) || defined(RPGPU_DIAG_NO_LOOKUP)  // keep verdicts OK
@@ -456,13 +447,13 @@ __global__ __launch_bounds__(kValidateThreads) void validate_kernel(
     sp.prev = __builtin_amdgcn_s_memtime();
 #endif
     Prefetch pf;
-    pf.gm = Geom{0, 0, 0};
+    pf.gm = Geom{0, 0};
     if (gw < n) {
         const rpgpu_batch_desc d0 = sload_desc(descs + gw);
         const uint8_t* p0 = data + d0.offset;
         const __amdgpu_buffer_rsrc_t rs0 = batch_rsrc(p0);
         pf.hv = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs0, (int32_t)(4 * (lane_id() & 15)), 0, 0);
-        pf.gm = desc_geometry(d0, data);
+        pf.gm = desc_geometry(d0);
         load_rows(pf.x, rs0, pf.gm, 0, lane_id());
     }
     for (uint32_t g = gw; g < n; g += kGroup * nw) {

@@ -11,8 +11,8 @@
 //   W[s]  = S_{-16*2^s} split into 8 nibble tables (butterfly combine);
 //   H     = S_{-960} as 8 nibble tables (header-CRC window correction);
 //   T0    = the plain byte table;
-//   P[p]  = S_{-p}, p = 0..15, as nibble tables (drops the zero pad that
-//           extends a batch's CRC region to a 16-byte aligned end).
+//   U[m]  = S_{-1024*m}, m < kRowsPerChunk, as nibble tables (removes the
+//           m all-zero "phantom" rows that round a batch up to whole chunks).
 #include <stdint.h>
 #include <string.h>
 
@@ -68,7 +68,7 @@ void build_tables(uint32_t* out) {
     }
     for (int s = 0; s < 6; s++) nibble_tables(-16ll * (1ll << s), out + kOffW + s * 128);
     nibble_tables(-960, out + kOffH);
-    for (int p = 0; p < 16; p++) nibble_tables(-p, out + kOffP + p * 128);
+    for (int m = 0; m < kRowsPerChunk; m++) nibble_tables(-1024ll * m, out + kOffU + m * 128);
 }
 
 }  // namespace rpgpu
