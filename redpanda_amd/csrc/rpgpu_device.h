@@ -51,6 +51,13 @@ __device__ __forceinline__ uint32_t lane_id() {
     return r;
 }
 __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+// v with lane L replaced by the wave-uniform value s
+template <class S>
+__device__ __forceinline__ uint32_t writelane_impl(uint32_t v, uint32_t s, int lane) {
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(__builtin_amdgcn_readfirstlane(s)), "i"(lane));
+    return v;
+}
+#define writelane(v, s, L) writelane_impl<void>((v), (s), (L))
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
 // order this wave's LDS writes before its later LDS reads by other lanes

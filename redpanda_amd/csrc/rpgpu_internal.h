@@ -19,11 +19,14 @@ constexpr int64_t kHcountLimit = 1ll << 20;
 // LDS bank (16 entries sit in 16 distinct banks).
 constexpr int kOffN = 0;                 // 32 x 16: block nibble tables, pre-shifted 1008 B
 constexpr int kOffW = kOffN + 32 * 16;   // 6 x 8 x 16: x^(-8*16*2^s), nibble tables
-constexpr int kOffH = kOffW + 6 * 128;   // 8 x 16: x^(-8*960), nibble tables
-constexpr int kOffT0 = kOffH + 128;      // 256: plain byte table (ranges shorter than 4 B)
+constexpr int kOffT0 = kOffW + 6 * 128;  // 256: plain byte table (ranges shorter than 4 B)
 constexpr int kRowsPerChunk = 8;        // 8 x 1 KiB rows in flight per wave
 constexpr int kOffU = kOffT0 + 256;      // kRowsPerChunk x 8 x 16: x^(-8*1024*m) (phantom rows)
-constexpr int kTableWords = kOffU + kRowsPerChunk * 128;
+// 2 x 16 x 64: header-CRC tables, one byte of a 64-byte window per lane:
+// word (h * 16 + v) * 64 + l = S_{63-l}(T0[v << 4h]).  Lane l always reads
+// bank l mod 32, so the lookups never conflict.
+constexpr int kOffHB = kOffU + kRowsPerChunk * 128;
+constexpr int kTableWords = kOffHB + 2 * 16 * 64;
 static_assert(kTableWords % 4 == 0, "table blob is copied as 16-byte words");
 
 constexpr int kValidateThreads = 256;  // 4 waves per workgroup

@@ -56,7 +56,7 @@ struct Stamps {
 struct Header {
     int32_t size_bytes;
     int64_t base_offset;
-    int8_t type;
+    int32_t type;  // int8 in the reference; kept 32-bit so the struct has no padding
     int32_t crc;
     int16_t attrs;
     int32_t last_offset_delta;
@@ -72,17 +72,21 @@ struct Result {
     uint32_t index_first, index_count;
 };
 
+// Every dword goes through readfirstlane (the values are wave-uniform): this
+// keeps the SLP vectorizer from turning the field reads into vector loads of
+// the struct, which would force the struct into scratch memory.
+__device__ __forceinline__ uint32_t u32s(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ void write_result(rpgpu_batch_result* out, const Result& r) {
     if (lane_id() == 0) {
-        u32x4 a = {(uint32_t)r.verdict, r.crc, r.crc_expected, r.header_crc};
-        u32x4 b = {(uint32_t)r.h.size_bytes, (uint32_t)r.h.record_count, (uint32_t)(uint64_t)r.h.base_offset,
-                   (uint32_t)((uint64_t)r.h.base_offset >> 32)};
-        u32x4 c = {(uint32_t)r.h.last_offset_delta,
-                   (uint32_t)(uint16_t)r.h.attrs | ((uint32_t)(r.h.attrs & 7) << 16) |
-                       ((uint32_t)(uint8_t)r.h.type << 24),
-                   (uint32_t)(uint64_t)r.h.first_ts, (uint32_t)((uint64_t)r.h.first_ts >> 32)};
-        u32x4 d = {(uint32_t)(uint64_t)r.h.max_ts, (uint32_t)((uint64_t)r.h.max_ts >> 32), r.index_first,
-                   r.index_count};
+        const uint64_t bo = (uint64_t)r.h.base_offset, ft = (uint64_t)r.h.first_ts, mt = (uint64_t)r.h.max_ts;
+        u32x4 a = {u32s((uint32_t)r.verdict), u32s(r.crc), u32s(r.crc_expected), u32s(r.header_crc)};
+        u32x4 b = {u32s((uint32_t)r.h.size_bytes), u32s((uint32_t)r.h.record_count), u32s((uint32_t)bo),
+                   u32s((uint32_t)(bo >> 32))};
+        u32x4 c = {u32s((uint32_t)r.h.last_offset_delta),
+                   u32s((uint32_t)(uint16_t)r.h.attrs | ((uint32_t)(r.h.attrs & 7) << 16) |
+                        ((uint32_t)(uint8_t)r.h.type << 24)),
+                   u32s((uint32_t)ft), u32s((uint32_t)(ft >> 32))};
+        u32x4 d = {u32s((uint32_t)mt), u32s((uint32_t)(mt >> 32)), u32s(r.index_first), u32s(r.index_count)};
         u32x4* o = reinterpret_cast<u32x4*>(out);
         o[0] = a;
         o[1] = b;
@@ -98,8 +102,10 @@ __device__ __forceinline__ void load_tables(uint32_t* s, const uint32_t* __restr
 }
 
 // header CRC over image D[4..61) (internal_header_only_crc,
-// record_utils.cc:34-55): lanes 0..3 take the 64-byte right-aligned window
-// [7 zero bytes | D[4..61)], init folded into D[4..8).
+// record_utils.cc:34-55): the 64-byte right-aligned window
+// [7 zero bytes | D[4..61)], init folded into D[4..8), one byte per lane
+// through the lane-minor tables HB (2 conflict-free lookups), then an XOR
+// reduction over the wave.
 __device__ __forceinline__ uint32_t header_crc_vec(const uint32_t* sT, const Img64& D) {
     uint32_t win[16];
     win[0] = 0;
@@ -108,17 +114,21 @@ __device__ __forceinline__ uint32_t header_crc_vec(const uint32_t* sT, const Img
 #pragma unroll
     for (int m = 3; m < 16; m++) win[m] = (D.w[m - 1] >> 8) | (D.w[m] << 24);
     const uint32_t l = lane_id();
-    u32x4 blk = {0, 0, 0, 0};
+    // lane i < 16 holds window dword i (writelane, not a select over an
+    // array: that would be lowered to scratch memory), then every lane
+    // fetches the dword of its byte
+    uint32_t vwin = 0;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        if (l == (uint32_t)j) blk = (u32x4){win[4 * j], win[4 * j + 1], win[4 * j + 2], win[4 * j + 3]};
-    }
-    uint32_t c = crc_block(sT + kOffN, blk);
-    const uint32_t* sW = sT + kOffW;
-    c ^= apply8(sW + 0 * 128, row_shl<1>(c));
-    c ^= apply8(sW + 1 * 128, row_shl<2>(c));
-    c = apply8(sT + kOffH, c);
-    return ~rdl(c, 0);
+    for (int i = 0; i < 16; i++) vwin = writelane(vwin, win[i], i);
+    const uint32_t w = __builtin_amdgcn_ds_bpermute((int)((l >> 2) << 2), vwin);
+    const uint32_t byte = (w >> (8 * (l & 3))) & 255u;
+    const uint32_t* hb = sT + kOffHB + l;
+    uint32_t c = hb[(byte & 15u) * 64] ^ hb[(16u + (byte >> 4)) * 64];
+    c ^= row_shl<1>(c);
+    c ^= row_shl<2>(c);
+    c ^= row_shl<4>(c);
+    c ^= row_shl<8>(c);
+    return ~(rdl(c, 0) ^ rdl(c, 16) ^ rdl(c, 32) ^ rdl(c, 48));
 }
 
 // Row geometry of the CRC region [21, n) of a batch: 1 KiB rows aligned to
@@ -217,7 +227,10 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
     Result r;
     r.verdict = RPGPU_V_OK;
     r.crc = r.crc_expected = r.header_crc = 0;
-    r.h = Header{};
+    r.h.size_bytes = r.h.type = r.h.crc = r.h.last_offset_delta = 0;
+    r.h.base_sequence = r.h.record_count = 0;
+    r.h.attrs = r.h.producer_epoch = 0;
+    r.h.base_offset = r.h.first_ts = r.h.max_ts = r.h.producer_id = 0;
     r.index_first = index_first;
     r.index_count = 0;
 
@@ -464,8 +477,10 @@ __global__ __launch_bounds__(kValidateThreads) void validate_kernel(
             if (b >= n) break;
             const rpgpu_batch_desc d = sload_desc(descs + b);
             const bool has_next = b + nw < n;
-            rpgpu_batch_desc nd{};
-            if (has_next) nd = sload_desc(descs + b + nw);
+            // always loaded (the batch's own descriptor when there is no
+            // next one; has_next masks its use): a conditionally initialised
+            // struct is lowered to scratch memory
+            const rpgpu_batch_desc nd = sload_desc(descs + (has_next ? b + nw : b));
             const uint64_t first = sload(block_base + b / kScanBlock) + sload(local_first + b);
             // never write past the caller's index buffer (rpgpu_validate_device)
             uint64_t cap = sload(caps + b);

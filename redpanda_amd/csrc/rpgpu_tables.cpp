@@ -9,10 +9,11 @@
 //           by the block's remaining 15-i bytes and the 1008-byte gap to the
 //           lane's next block: S_{15-i+1008} o T0 restricted to that nibble;
 //   W[s]  = S_{-16*2^s} split into 8 nibble tables (butterfly combine);
-//   H     = S_{-960} as 8 nibble tables (header-CRC window correction);
 //   T0    = the plain byte table;
 //   U[m]  = S_{-1024*m}, m < kRowsPerChunk, as nibble tables (removes the
-//           m all-zero "phantom" rows that round a batch up to whole chunks).
+//           m all-zero "phantom" rows that round a batch up to whole chunks);
+//   HB[h][v][l] = S_{63-l}(T0[v << 4h]): byte l of a 64-byte window, one
+//           lane per byte (header CRC), laid out lane-minor.
 #include <stdint.h>
 #include <string.h>
 
@@ -67,8 +68,15 @@ void build_tables(uint32_t* out) {
         }
     }
     for (int s = 0; s < 6; s++) nibble_tables(-16ll * (1ll << s), out + kOffW + s * 128);
-    nibble_tables(-960, out + kOffH);
     for (int m = 0; m < kRowsPerChunk; m++) nibble_tables(-1024ll * m, out + kOffU + m * 128);
+    for (int l = 0; l < 64; l++) {
+        uint32_t basis[32];
+        shift_basis(63 - l, basis);
+        for (uint32_t v = 0; v < 16; v++) {
+            out[kOffHB + (0 * 16 + v) * 64 + l] = apply_basis(basis, t0[v]);
+            out[kOffHB + (1 * 16 + v) * 64 + l] = apply_basis(basis, t0[v << 4]);
+        }
+    }
 }
 
 }  // namespace rpgpu
