@@ -54,6 +54,10 @@ enum rpgpu_op {
     RPGPU_OP_PARSE = 1u << 2,  /* record field walk (uncompressed batches)*/
     RPGPU_OP_INDEX = 1u << 3,  /* emit per-record index entries           */
     RPGPU_OP_DECOMP = 1u << 4, /* decompress compressed bodies            */
+    /* on-disk batches only: compute crc and header_crc instead of checking
+     * them (reset_size_checksum_metadata, storage/parser_utils.cc:122-128);
+     * used for the rewritten batches of rpgpu_decomp_run_device */
+    RPGPU_OP_RECRC = 1u << 5,
 };
 #define RPGPU_OPS_PRODUCE (RPGPU_OP_CRC | RPGPU_OP_HDRCRC | RPGPU_OP_PARSE | RPGPU_OP_INDEX)
 
@@ -85,6 +89,8 @@ enum rpgpu_verdict {
     RPGPU_V_LZ4_TRAILING = 32,     /* unconsumed input after LZ4 frame end        */
     RPGPU_V_DECOMP_UNSUPPORTED = 33,/* codec not implemented on this engine (gzip) */
     RPGPU_V_DECOMP_OVERFLOW = 34,  /* decompressed size exceeds the output slot   */
+    RPGPU_V_SKIPPED = 40,          /* not decompressed: no RPGPU_OP_DECOMP, not
+                                      validated OK, or not compressed        */
 };
 
 /* Produce-path mapping of verdicts to Kafka error codes
@@ -242,6 +248,61 @@ uint32_t rpgpu_crc32c_extend(rpgpu_ctx* ctx, uint32_t crc, const void* p, size_t
 uint32_t rpgpu_internal_header_only_crc(rpgpu_ctx* ctx, const rpgpu_rp_header* h);
 int32_t rpgpu_crc_record_batch(rpgpu_ctx* ctx, const rpgpu_rp_header* h,
                                const void* body, size_t n);
+
+/* ---- decompression (storage read path) ---------------------------------
+ * Replaces, per compressed batch,
+ *   compression::compressor::uncompress            compression/compression.cc:35-55
+ *     lz4_frame_compressor::uncompress             compression/internal/lz4_frame_compressor.cc:160-278
+ *     snappy_java_compressor::uncompress           compression/internal/snappy_java_compressor.cc:76-110
+ *   storage::internal::maybe_decompress_batch_sync storage/parser_utils.cc:52-68,122-128
+ * and walks / indexes the records of the decompressed batch
+ * (model/record.h:668-691).  zstd and gzip are not decoded yet:
+ * RPGPU_V_DECOMP_UNSUPPORTED.
+ *
+ * A batch is decompressed when its descriptor has RPGPU_OP_DECOMP, its
+ * validation verdict (d_results of rpgpu_run_device / rpgpu_validate_device
+ * over the same arena) is RPGPU_V_OK and its codec is not none; every other
+ * batch reports RPGPU_V_SKIPPED.  For each decompressed batch the output
+ * buffer receives the rewritten on-disk batch (little-endian 61-byte header +
+ * body) at out_offset: codec bits removed, size_bytes = 61 + out_len,
+ * crc = crc_record_batch over the decompressed body, header_crc =
+ * internal_header_only_crc.  A truncated frame yields the partial output with
+ * RPGPU_V_OK, as the reference does. */
+typedef struct rpgpu_decomp_result {
+    int32_t verdict;     /* OK, DECOMP_ERROR, LZ4_TRAILING, DECOMP_UNSUPPORTED,
+                            DECOMP_OVERFLOW, REC_UNDEFINED (snappy-java chunk
+                            length with bit 31 set), SKIPPED                  */
+    uint32_t codec;      /* attrs & 7 of the input batch                      */
+    uint64_t out_offset; /* rewritten batch in the output buffer              */
+    uint64_t out_len;    /* decompressed body bytes                           */
+    uint64_t out_cap;    /* bytes reserved for the batch (header + bound of
+                            the decoded size + slack)                         */
+} rpgpu_decomp_result;   /* 32 bytes */
+
+size_t rpgpu_decomp_scratch_bytes(uint32_t n);
+/* Plan: per-batch output slots and their exclusive scan into d_scratch;
+ * *d_out_bytes = output bytes needed.  The output buffer must hold
+ * *d_out_bytes + RPGPU_ARENA_TAIL_PAD bytes. */
+int32_t rpgpu_decomp_plan_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_descs, uint32_t n,
+                                 const uint8_t* d_data, const rpgpu_batch_result* d_results,
+                                 uint64_t* d_out_bytes, void* d_scratch, void* hip_stream);
+/* Run (needs the plan, same d_scratch): decode, rewrite, then validate, walk
+ * and index the rewritten batches.  d_out_descs[i] / d_out_results[i]
+ * describe rewritten batch i (length 0, ops 0, verdict STREAM_SHORT where
+ * nothing was decompressed); index entries are laid out as by
+ * rpgpu_run_device over d_out_descs; *d_index_used = entries reserved. */
+int32_t rpgpu_decomp_run_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_descs, uint32_t n,
+                                const uint8_t* d_data, const rpgpu_batch_result* d_results,
+                                rpgpu_decomp_result* d_dres, uint8_t* d_out, uint64_t out_cap,
+                                rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_out_results,
+                                rpgpu_record_index* d_index, uint64_t index_cap,
+                                uint64_t* d_index_used, void* d_scratch, void* hip_stream);
+/* Synchronous scalar mirror of compression::compressor::uncompress(buf, codec)
+ * on the GPU, host buffers.  Returns the verdict (>= 0) or a negative status;
+ * *out_len = decompressed bytes (the size needed when the verdict is
+ * RPGPU_V_DECOMP_OVERFLOW; `out` then holds the first `cap` bytes). */
+int32_t rpgpu_uncompress(rpgpu_ctx* ctx, int32_t codec, const void* in, size_t n, void* out,
+                         size_t cap, size_t* out_len);
 
 #ifdef __cplusplus
 }

@@ -31,7 +31,7 @@ _L = None
 
 
 def build(force: bool = False) -> Path:
-    srcs = [HERE / f for f in ("crc32c.c", "batch.c", "codec.c", "rporacle.h", "Makefile")]
+    srcs = [HERE / f for f in ("crc32c.c", "batch.c", "codec.c", "decomp.c", "rporacle.h", "Makefile")]
     if force or not LIB_PATH.exists() or any(s.stat().st_mtime > LIB_PATH.stat().st_mtime for s in srcs):
         r = subprocess.run(["make", "-C", str(HERE), "-s"], capture_output=True, text=True)
         if r.returncode != 0:
@@ -70,6 +70,8 @@ def lib() -> C.CDLL:
         L.orc_compress.argtypes = [C.c_int, vp, sz, vp, sz, C.POINTER(sz)]
         L.orc_compress_bound.restype = sz
         L.orc_compress_bound.argtypes = [C.c_int, sz]
+        L.orc_decompress_batches.restype = None
+        L.orc_decompress_batches.argtypes = [vp, u32, vp, vp, u32, vp, vp, vp, vp, vp, vp, C.c_int]
         _L = L
     return _L
 
@@ -146,3 +148,35 @@ def compress(codec: int, data) -> bytes:
     if v != 0:
         raise RuntimeError(f"compress({codec}) -> {v}")
     return out[: n.value].tobytes()
+
+
+def decompress_arena(data: np.ndarray, descs: np.ndarray, results: np.ndarray, caps,
+                     codecs=(2, 3), nthreads: int = 1) -> dict:
+    """Reference outcome of the decompress path for an arena already validated
+    (`results` = validate_arena's or the engine's validation results, which
+    agree): storage::internal::maybe_decompress_batch_sync
+    (storage/parser_utils.cc:52-68,122-128) per batch with RPGPU_OP_DECOMP,
+    verdict OK and a codec, then the rewritten batches through validate_arena
+    as on-disk batches.  caps[i] = decoded-body capacity for batch i; codecs
+    outside `codecs` report RPGPU_V_DECOMP_UNSUPPORTED (33), as the engine
+    does for zstd/gzip."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    descs = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+    results = np.ascontiguousarray(results, dtype=RESULT_DTYPE)
+    n = len(descs)
+    caps = np.ascontiguousarray(caps, dtype=np.uint64)
+    slots = (61 + caps + 64 + 15) & ~np.uint64(15)
+    offs = np.zeros(n, dtype=np.uint64)
+    if n:
+        offs[1:] = np.cumsum(slots)[:-1]
+    out = np.zeros(int(slots.sum()) + 64, dtype=np.uint8)
+    verdicts = np.zeros(n, dtype=np.int32)
+    lens = np.zeros(n, dtype=np.uint64)
+    rdescs = np.zeros(n, dtype=DESC_DTYPE)
+    mask = sum(1 << c for c in codecs)
+    lib().orc_decompress_batches(descs.ctypes.data, n, data.ctypes.data, results.ctypes.data, mask,
+                                 out.ctypes.data, offs.ctypes.data, caps.ctypes.data,
+                                 verdicts.ctypes.data, lens.ctypes.data, rdescs.ctypes.data, nthreads)
+    rres, ridx, rused = validate_arena(out, rdescs, nthreads=nthreads)
+    return dict(verdicts=verdicts, out_len=lens, out=out, out_descs=rdescs, out_results=rres,
+                index=ridx, used=rused)

@@ -79,6 +79,18 @@ int32_t orc_compress(int codec, const uint8_t* in, size_t n, uint8_t* out,
                      size_t cap, size_t* out_len);
 size_t orc_compress_bound(int codec, size_t n);
 
+/* storage::internal::maybe_decompress_batch_sync (storage/parser_utils.cc:52-68,
+ * 122-128) for every batch with RPGPU_OP_DECOMP whose validation result `vres`
+ * is OK and whose codec is set (codecs outside codec_mask, a bit per codec:
+ * RPGPU_V_DECOMP_UNSUPPORTED; other batches RPGPU_V_SKIPPED): body decoded to
+ * out + out_off[i] + 61 (at most out_cap[i] bytes), rewritten LE header at
+ * out + out_off[i], rdescs[i] = the rewritten on-disk batch (length 0, ops 0
+ * when nothing was decompressed) for orc_validate_arena. */
+void orc_decompress_batches(const rpgpu_batch_desc* descs, uint32_t n, const uint8_t* data,
+                            const rpgpu_batch_result* vres, uint32_t codec_mask, uint8_t* out,
+                            const uint64_t* out_off, const uint64_t* out_cap, int32_t* verdicts,
+                            uint64_t* out_len, rpgpu_batch_desc* rdescs, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,6 +22,7 @@ OP_HDRCRC = 2
 OP_PARSE = 4
 OP_INDEX = 8
 OP_DECOMP = 16
+OP_RECRC = 32
 OPS_PRODUCE = OP_CRC | OP_HDRCRC | OP_PARSE | OP_INDEX
 
 V_OK = 0
@@ -44,6 +45,7 @@ V_DECOMP_BAD_ALLOC = 31
 V_LZ4_TRAILING = 32
 V_DECOMP_UNSUPPORTED = 33
 V_DECOMP_OVERFLOW = 34
+V_SKIPPED = 40
 
 VERDICT_NAMES = {v: k for k, v in globals().items() if k.startswith("V_") and isinstance(v, int)}
 
@@ -69,7 +71,9 @@ RP_HEADER_DTYPE = np.dtype([("header_crc", "<u4"), ("size_bytes", "<i4"), ("base
                             ("max_timestamp", "<i8"), ("producer_id", "<i8"),
                             ("producer_epoch", "<i2"), ("base_sequence", "<i4"),
                             ("record_count", "<i4")])
-assert DESC_DTYPE.itemsize == 24 and RESULT_DTYPE.itemsize == 64
+DECOMP_RESULT_DTYPE = np.dtype([("verdict", "<i4"), ("codec", "<u4"), ("out_offset", "<u8"),
+                                ("out_len", "<u8"), ("out_cap", "<u8")])
+assert DESC_DTYPE.itemsize == 24 and RESULT_DTYPE.itemsize == 64 and DECOMP_RESULT_DTYPE.itemsize == 32
 assert INDEX_DTYPE.itemsize == 32 and RP_HEADER_DTYPE.itemsize == 61
 
 # ---- batch builder spec (redpanda_amd/csrc/rpgen.h) -------------------------
@@ -137,6 +141,12 @@ def lib() -> C.CDLL:
         _sig(L.rpgpu_crc32c_extend, _u32, _vp, _u32, _vp, C.c_size_t)
         _sig(L.rpgpu_internal_header_only_crc, _u32, _vp, _vp)
         _sig(L.rpgpu_crc_record_batch, _i32, _vp, _vp, _vp, C.c_size_t)
+        _sig(L.rpgpu_decomp_scratch_bytes, C.c_size_t, _u32)
+        _sig(L.rpgpu_decomp_plan_device, _i32, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp)
+        _sig(L.rpgpu_decomp_run_device, _i32, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp,
+             _u64, _vp, _vp, _vp)
+        _sig(L.rpgpu_uncompress, _i32, _vp, _i32, _vp, C.c_size_t, _vp, C.c_size_t,
+             C.POINTER(C.c_size_t))
         _LIB = L
     return _LIB
 
@@ -162,4 +172,6 @@ EXPORTED = [
     "rpgpu_validate_scratch_bytes", "rpgpu_validate_device", "rpgpu_plan_device",
     "rpgpu_run_device", "rpgpu_crc32c_ranges_device",
     "rpgpu_crc32c_extend", "rpgpu_internal_header_only_crc", "rpgpu_crc_record_batch",
+    "rpgpu_decomp_scratch_bytes", "rpgpu_decomp_plan_device", "rpgpu_decomp_run_device",
+    "rpgpu_uncompress",
 ]

@@ -32,6 +32,19 @@ hipError_t launch_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_
 hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                       rpgpu_batch_result* d_res, rpgpu_record_index* d_index, uint64_t index_cap,
                       const void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s);
+size_t decomp_scratch_bytes(uint32_t n);
+hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
+                              const rpgpu_batch_result* d_vres, uint64_t* d_out_bytes, void* d_scratch,
+                              hipStream_t s);
+hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
+                             const rpgpu_batch_result* d_vres, rpgpu_decomp_result* d_dres, uint8_t* d_out,
+                             uint64_t out_cap, rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_vres2,
+                             rpgpu_record_index* d_index, uint64_t index_cap, uint64_t* d_index_used,
+                             void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s);
+hipError_t launch_uncompress_bound(uint32_t codec, const uint8_t* d_in, uint64_t n, uint64_t* d_res,
+                                   hipStream_t s);
+hipError_t launch_uncompress_one(uint32_t codec, const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint64_t cap,
+                                 uint64_t* d_res, hipStream_t s);
 }  // namespace rpgpu
 
 namespace {
@@ -78,6 +91,7 @@ struct rpgpu_ctx {
     uint32_t* d_tables = nullptr;
     DevBuf work;     // submissions: descs | data | results | index | scratch | used
     DevBuf small;    // scalar mirrors
+    DevBuf small_out;  // scalar mirrors: decompression output
     std::vector<Ticket> tickets;
     uint64_t next_ticket = 1;
     bool busy = false;  // one in-flight submission per context (shard-owned)
@@ -113,8 +127,8 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
         return nullptr;
     }
     c->cu_count = prop.multiProcessorCount;
-    // kBlocksPerCU 4-wave workgroups per CU (RPGPU_BLOCKS_PER_CU overrides,
-    // for tuning runs)
+    // kBlocksPerCU workgroups per CU (RPGPU_BLOCKS_PER_CU overrides, for
+    // tuning runs)
     int bpc = rpgpu::kBlocksPerCU;
     if (const char* e = getenv("RPGPU_BLOCKS_PER_CU")) {
         const int v = atoi(e);
@@ -147,6 +161,7 @@ void rpgpu_close(rpgpu_ctx* c) {
     }
     c->work.release();
     c->small.release();
+    c->small_out.release();
     if (c->d_tables) (void)hipFree(c->d_tables);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -206,6 +221,35 @@ int32_t rpgpu_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, uint32_t
     hipError_t e = rpgpu::launch_run(d_descs, n, d_data, d_results, d_index, d_index ? index_cap : 0,
                                      d_scratch, c->d_tables, c->grid, s);
     if (e != hipSuccess) return fail(c, e, "run launch");
+    return RPGPU_OK;
+}
+
+size_t rpgpu_decomp_scratch_bytes(uint32_t n) { return rpgpu::decomp_scratch_bytes(n); }
+
+int32_t rpgpu_decomp_plan_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, uint32_t n,
+                                 const uint8_t* d_data, const rpgpu_batch_result* d_results,
+                                 uint64_t* d_out_bytes, void* d_scratch, void* hip_stream) {
+    if (!c || (n && (!d_descs || !d_data || !d_results || !d_scratch))) return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_decomp_plan(d_descs, n, d_data, d_results, d_out_bytes, d_scratch, s);
+    if (e != hipSuccess) return fail(c, e, "decomp plan launch");
+    return RPGPU_OK;
+}
+
+int32_t rpgpu_decomp_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, uint32_t n,
+                                const uint8_t* d_data, const rpgpu_batch_result* d_results,
+                                rpgpu_decomp_result* d_dres, uint8_t* d_out, uint64_t out_cap,
+                                rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_out_results,
+                                rpgpu_record_index* d_index, uint64_t index_cap,
+                                uint64_t* d_index_used, void* d_scratch, void* hip_stream) {
+    if (!c || (n && (!d_descs || !d_data || !d_results || !d_dres || !d_out || !d_out_descs ||
+                     !d_out_results || !d_scratch)))
+        return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_decomp_run(d_descs, n, d_data, d_results, d_dres, d_out, out_cap, d_out_descs,
+                                            d_out_results, d_index, d_index ? index_cap : 0, d_index_used,
+                                            d_scratch, c->d_tables, c->grid, s);
+    if (e != hipSuccess) return fail(c, e, "decomp run launch");
     return RPGPU_OK;
 }
 
@@ -363,6 +407,46 @@ static int32_t crc_one(rpgpu_ctx* c, uint32_t seed, const void* p, size_t n, uin
         (e = hipStreamSynchronize(c->stream)) != hipSuccess)
         return fail(c, e, "download");
     return RPGPU_OK;
+}
+
+// compression::compressor::uncompress (compression/compression.cc:35-55) for
+// one buffer: bound and decode on the GPU (rpgpu_decomp.hip), then copy back
+int32_t rpgpu_uncompress(rpgpu_ctx* c, int32_t codec, const void* in, size_t n, void* out, size_t cap,
+                         size_t* out_len) {
+    if (!c || (n && !in) || !out_len || (cap && !out) || codec < 0) return RPGPU_EINVAL;
+    *out_len = 0;
+    (void)hipSetDevice(c->device);
+    const size_t o_meta = align_up(n + RPGPU_ARENA_TAIL_PAD, 256);
+    hipError_t e = c->small.reserve(o_meta + 64);
+    if (e != hipSuccess) return fail(c, e, "device buffer");
+    uint8_t* base = static_cast<uint8_t*>(c->small.p);
+    uint64_t* meta = reinterpret_cast<uint64_t*>(base + o_meta);
+    uint64_t h[3] = {0, 0, 0};
+    if ((n && (e = hipMemcpyAsync(base, in, n, hipMemcpyHostToDevice, c->stream)) != hipSuccess) ||
+        (e = hipMemsetAsync(base + n, 0, RPGPU_ARENA_TAIL_PAD, c->stream)) != hipSuccess)
+        return fail(c, e, "upload");
+    if ((e = rpgpu::launch_uncompress_bound((uint32_t)codec, base, n, meta, c->stream)) != hipSuccess)
+        return fail(c, e, "bound launch");
+    if ((e = hipMemcpyAsync(h, meta, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        return fail(c, e, "download");
+    const uint64_t bound = h[0];
+    if ((e = c->small_out.reserve(bound + 256)) != hipSuccess) return fail(c, e, "device buffer");
+    uint8_t* dout = static_cast<uint8_t*>(c->small_out.p);
+    if ((e = rpgpu::launch_uncompress_one((uint32_t)codec, base, n, dout, bound, meta, c->stream)) != hipSuccess)
+        return fail(c, e, "uncompress launch");
+    if ((e = hipMemcpyAsync(h, meta, sizeof(h), hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        return fail(c, e, "download");
+    int32_t verdict = (int32_t)(int64_t)h[1];
+    const uint64_t len = h[2];
+    const uint64_t ncopy = len < cap ? len : cap;
+    if (ncopy && ((e = hipMemcpyAsync(out, dout, ncopy, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+                  (e = hipStreamSynchronize(c->stream)) != hipSuccess))
+        return fail(c, e, "download");
+    if (verdict == RPGPU_V_OK && len > cap) verdict = RPGPU_V_DECOMP_OVERFLOW;
+    *out_len = len;
+    return verdict;
 }
 
 uint32_t rpgpu_crc32c_extend(rpgpu_ctx* c, uint32_t crc, const void* p, size_t n) {

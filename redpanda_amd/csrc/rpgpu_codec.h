@@ -1,0 +1,629 @@
+// rpgpu_codec.h — per-lane decoders for compressed record bodies: LZ4 frame
+// and snappy-java / raw snappy, one lane per batch.
+//
+// Each decoder restates, for one contiguous input buffer, the reference's
+// wrapper loop around its codec library together with the library's own
+// acceptance rules, so that decoded bytes AND verdicts match on corrupt input
+// too (the oracle is the reference's wrapper over the image's
+// liblz4 1.9.3 / snappy 1.1.8, oracle/codec.c):
+//   LZ4    compression/internal/lz4_frame_compressor.cc:160-278 over
+//          LZ4F_getFrameInfo / LZ4F_decompress / LZ4_decompress_safe_usingDict
+//          (lz4frame.c, lz4.c of liblz4 1.9.3, LZ4_FAST_DEC_LOOP as built for
+//          x86-64)
+//   snappy compression/internal/snappy_java_compressor.cc:76-110 ->
+//          compression/snappy_standard_compressor.cc:102-160 over
+//          snappy::GetUncompressedLength / snappy::RawUncompress (snappy 1.1.8)
+//   dispatch compression/compression.cc:35-55
+//
+// Plain C++: the same code runs on the device (rpgpu_decomp.hip) and on the
+// host in the differential fuzz test against the oracle
+// (tests/native/codec_fuzz.cpp).  Copies move up to 64 bytes per step and may
+// run up to 63 bytes past the end of a sequence (later sequences overwrite
+// those bytes, as liblz4's own wild copies do), so an output buffer needs
+// kSlack writable bytes past its planned capacity and an input buffer 64
+// readable bytes past its end (RPGPU_ARENA_TAIL_PAD).
+#ifndef RPGPU_CODEC_H
+#define RPGPU_CODEC_H
+
+#include <stdint.h>
+#include <string.h>
+
+#ifdef __HIPCC__
+#define RPC_HD __host__ __device__ __forceinline__
+#else
+#define RPC_HD static inline
+#endif
+
+namespace rpcodec {
+
+constexpr uint64_t kSlack = 128;
+constexpr uint64_t kMaxChunk = 128u * 1024u;  // details::io_allocation_size::max_chunk_size
+// verdicts (include/rpgpu.h)
+constexpr int32_t V_OK = 0, V_UNDEFINED = 11, V_ERROR = 30, V_TRAILING = 32, V_UNSUPPORTED = 33,
+                  V_OVERFLOW = 34;
+
+struct B16 {
+    uint32_t w[4];
+};
+RPC_HD void ld16(B16& v, const uint8_t* p) { __builtin_memcpy(&v, p, 16); }
+RPC_HD void st16(uint8_t* p, const B16& v) { __builtin_memcpy(p, &v, 16); }
+RPC_HD uint32_t le16(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+RPC_HD uint32_t le32(const uint8_t* p) {
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+}
+RPC_HD uint64_t le64(const uint8_t* p) {
+    uint64_t v;
+    __builtin_memcpy(&v, p, 8);
+    return v;
+}
+RPC_HD uint32_t be32(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+// dst[0, n) = src[0, n) for ranges that do not overlap within 64 bytes:
+// 64 bytes per step, four loads in flight
+RPC_HD void copy_fwd(uint8_t* dst, const uint8_t* src, uint64_t n) {
+    if (n <= 16) {
+        if (n) {
+            B16 v;
+            ld16(v, src);
+            st16(dst, v);
+        }
+        return;
+    }
+    for (uint64_t i = 0; i < n; i += 64) {
+        B16 a, b, c, d;
+        ld16(a, src + i);
+        ld16(b, src + i + 16);
+        ld16(c, src + i + 32);
+        ld16(d, src + i + 48);
+        st16(dst + i, a);
+        st16(dst + i + 16, b);
+        st16(dst + i + 32, c);
+        st16(dst + i + 48, d);
+    }
+}
+
+// LZ77 back-reference: dst[i] = dst[i - off] in increasing i, i.e. the
+// period-`off` extension of the `off` bytes before dst.  off == 0 yields
+// zeros, which is what liblz4's offset-0 copy produces (LZ4_write32(op, 0)
+// before the self-copy).
+RPC_HD void copy_match(uint8_t* dst, uint64_t off, uint64_t n) {
+    if (off >= 64) {
+        copy_fwd(dst, dst - off, n);  // each 64-byte source block is already written
+        return;
+    }
+    if (off >= 16) {
+        for (uint64_t i = 0; i < n; i += 16) {
+            B16 v;
+            ld16(v, dst - off + i);
+            st16(dst + i, v);
+        }
+        return;
+    }
+    // 16-byte pattern: the `off` bytes before dst repeated (two 64-bit
+    // halves, doubled by shifts; no per-byte array, which would live in
+    // scratch memory on the device)
+    uint64_t lo = 0, hi = 0, step = 16;
+    if (off != 0) {
+        const uint8_t* s = dst - off;
+        lo = le64(s);
+        hi = le64(s + 8);
+        if (off <= 8) {
+            if (off < 8) lo &= (1ull << (8 * off)) - 1;
+            hi = 0;
+        } else {
+            hi &= (1ull << (8 * (off - 8))) - 1;
+        }
+        for (uint64_t w = off; w < 16; w *= 2) {
+            const uint64_t sh = 8 * w;  // 8..120 bits
+            if (sh < 64) {
+                hi |= (hi << sh) | (lo >> (64 - sh));
+                lo |= lo << sh;
+            } else {
+                hi |= lo << (sh - 64);
+            }
+        }
+        step = off * (16 / off);  // a whole number of periods
+    }
+    B16 p;
+    p.w[0] = (uint32_t)lo;
+    p.w[1] = (uint32_t)(lo >> 32);
+    p.w[2] = (uint32_t)hi;
+    p.w[3] = (uint32_t)(hi >> 32);
+    for (uint64_t i = 0; i < n; i += step) st16(dst + i, p);
+}
+
+// ---------------------------------------------------------------- XXH32
+// xxhash.c XXH32 (one shot; the frame decoder's streaming states hash
+// contiguous data here, which gives the same digest)
+constexpr uint32_t kP1 = 2654435761u, kP2 = 2246822519u, kP3 = 3266489917u, kP4 = 668265263u,
+                   kP5 = 374761393u;
+RPC_HD uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+RPC_HD uint32_t xxh32(const uint8_t* p, uint64_t len, uint32_t seed) {
+    const uint8_t* const e = p + len;
+    uint32_t h;
+    if (len >= 16) {
+        uint32_t v1 = seed + kP1 + kP2, v2 = seed + kP2, v3 = seed, v4 = seed - kP1;
+        const uint8_t* const lim = e - 16;
+        do {
+            v1 = rotl32(v1 + le32(p) * kP2, 13) * kP1;
+            v2 = rotl32(v2 + le32(p + 4) * kP2, 13) * kP1;
+            v3 = rotl32(v3 + le32(p + 8) * kP2, 13) * kP1;
+            v4 = rotl32(v4 + le32(p + 12) * kP2, 13) * kP1;
+            p += 16;
+        } while (p <= lim);
+        h = rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18);
+    } else {
+        h = seed + kP5;
+    }
+    h += (uint32_t)len;
+    while (p + 4 <= e) {
+        h += le32(p) * kP3;
+        h = rotl32(h, 17) * kP4;
+        p += 4;
+    }
+    while (p < e) {
+        h += (uint32_t)(*p) * kP5;
+        h = rotl32(h, 11) * kP1;
+        p++;
+    }
+    h ^= h >> 15;
+    h *= kP2;
+    h ^= h >> 13;
+    h *= kP3;
+    h ^= h >> 16;
+    return h;
+}
+
+// ---------------------------------------------------------------- LZ4 block
+// read_variable_length (lz4.c): the safe decoder always checks the loop
+// bound; err = 1 is initial_error, 2 is loop_error.
+RPC_HD uint32_t lz4_varlen(const uint8_t* in, int64_t& ip, int64_t lencheck, bool initial_check, int& err) {
+    uint32_t len = 0;  // U32 in lz4.c
+    err = 0;
+    if (initial_check && ip >= lencheck) {
+        err = 1;
+        return 0;
+    }
+    uint32_t s;
+    do {
+        s = in[ip++];
+        len += s;
+        if (ip >= lencheck) {
+            err = 2;
+            return len;
+        }
+    } while (s == 255);
+    return len;
+}
+
+// LZ4_decompress_generic (lz4.c, liblz4 1.9.3) in its endOnInputSize /
+// decode_full_block form: the fast loop while 64 bytes of output remain,
+// then the safe loop (with its two-stage shortcut) once any check sends the
+// decoder there.  Acceptance is the library's, check for check; the copies
+// are the sequential LZ77 semantics the library's wild copies implement.
+// `hist` = bytes of earlier frame output before `out` that matches may reach
+// (linked blocks; LZ4F keeps at least min(history, 64 KiB) as dictionary).
+// Returns the decoded size, or -1.
+RPC_HD int64_t lz4_block(const uint8_t* in, int64_t isz, uint8_t* out, int64_t ocap, int64_t hist) {
+    if (isz == 0) return -1;  // ocap (maxBlockSize) is never 0 here
+    const int64_t iend = isz, oend = ocap;
+    const bool check_off = hist < 65536;  // checkOffset: dictSize < 64 KB
+    int64_t ip = 0, op = 0, off = 0;
+    bool safe = oend < 64;  // FASTLOOP_SAFE_DISTANCE
+    int err;
+    for (;;) {
+        const uint32_t token = in[ip++];
+        int64_t len = token >> 4;
+        bool lit_checks;  // the literals go through safe_literal_copy
+        if (!safe) {
+            if (len == 15) {
+                len += lz4_varlen(in, ip, iend - 15, true, err);
+                if (err == 1) return -1;
+                lit_checks = op + len > oend - 32 || ip + len > iend - 32;
+            } else {
+                lit_checks = ip > iend - 17;
+            }
+            if (lit_checks) safe = true;
+        } else {
+            // two-stage shortcut: literal length 0..14 and room for 16 + 18 bytes
+            if (len != 15 && ip < iend - 16 && op <= oend - 32) {
+                copy_fwd(out + op, in + ip, (uint64_t)len);
+                op += len;
+                ip += len;
+                len = token & 15;
+                off = le16(in + ip);
+                ip += 2;
+                if (len != 15 && off >= 8 && off <= op + hist) {  // match >= lowPrefix
+                    copy_match(out + op, (uint64_t)off, (uint64_t)len + 4);
+                    op += len + 4;
+                    continue;
+                }
+                goto match;
+            }
+            if (len == 15) {
+                len += lz4_varlen(in, ip, iend - 15, true, err);
+                if (err == 1) return -1;
+            }
+            lit_checks = true;
+        }
+        if (lit_checks && (op + len > oend - 12 || ip + len > iend - 8)) {
+            // MFLIMIT / input parsing restriction: must be the last literals
+            if (ip + len != iend || op + len > oend) return -1;
+            copy_fwd(out + op, in + ip, (uint64_t)len);
+            return op + len;
+        }
+        copy_fwd(out + op, in + ip, (uint64_t)len);
+        ip += len;
+        op += len;
+        off = le16(in + ip);
+        ip += 2;
+        len = token & 15;
+    match:
+        if (len == 15) {
+            len += lz4_varlen(in, ip, iend - 4, false, err);  // iend - LASTLITERALS + 1
+            if (err) return -1;
+        }
+        len += 4;  // MINMATCH
+        if (!safe && op + len >= oend - 64) safe = true;  // goto safe_match_copy
+        if (check_off && off > op + hist) return -1;      // offset outside buffers
+        if (safe && op + len > oend - 5) return -1;       // last LASTLITERALS bytes are literals
+        copy_match(out + op, (uint64_t)off, (uint64_t)len);
+        op += len;
+    }
+}
+
+// ---------------------------------------------------------------- LZ4 frame
+enum { kLz4Error = 0, kLz4Partial = 1, kLz4Skip = 2, kLz4Frame = 3 };
+constexpr uint32_t kLz4Magic = 0x184D2204u, kLz4SkipMagic = 0x184D2A50u;
+constexpr uint64_t kLz4HeaderSizeMax = 19;  // LZ4F_HEADER_SIZE_MAX
+
+struct Lz4Frame {
+    int32_t kind;
+    uint32_t hlen;       // frame header bytes
+    uint32_t max_block;  // LZ4F_getBlockSize(blockSizeID)
+    bool linked, block_sum, content_sum;
+    uint64_t content;  // frameInfo.contentSize (0 = not given)
+};
+
+// LZ4F_getFrameInfo (LZ4F_headerSize + LZ4F_decodeHeader) when the input
+// holds LZ4F_HEADER_SIZE_MAX bytes, else LZ4F_decompress's
+// dstage_storeFrameHeader path, which decodes the first 7 bytes and waits
+// for the rest: a header cut short there is "partial" (no error, no output).
+RPC_HD Lz4Frame lz4f_header(const uint8_t* in, uint64_t n) {
+    Lz4Frame f;
+    f.kind = kLz4Error;
+    f.hlen = f.max_block = 0;
+    f.linked = f.block_sum = f.content_sum = false;
+    f.content = 0;
+    if (n < 7) {
+        f.kind = kLz4Partial;
+        return f;
+    }
+    const uint32_t magic = le32(in);
+    if ((magic & 0xFFFFFFF0u) == kLz4SkipMagic) {
+        f.kind = kLz4Skip;
+        return f;
+    }
+    if (magic != kLz4Magic) return f;  // frameType_unknown
+    const uint32_t flg = in[4];
+    if ((flg >> 1) & 1u) return f;          // reservedFlag_set
+    if (((flg >> 6) & 3u) != 1u) return f;  // headerVersion_wrong
+    const uint32_t fhs = 7 + ((flg >> 3) & 1u) * 8 + (flg & 1u) * 4;
+    if (n < fhs) {
+        f.kind = kLz4Partial;
+        return f;
+    }
+    const uint32_t bd = in[5];
+    if ((bd >> 7) & 1u) return f;  // reservedFlag_set
+    const uint32_t bsid = (bd >> 4) & 7u;
+    if (bsid < 4) return f;  // maxBlockSize_invalid
+    if (bd & 15u) return f;  // reservedFlag_set
+    if (((xxh32(in + 4, fhs - 5, 0) >> 8) & 0xFFu) != in[fhs - 1]) return f;  // headerChecksum_invalid
+    f.kind = kLz4Frame;
+    f.hlen = fhs;
+    f.max_block = 1u << (8 + 2 * bsid);
+    f.linked = ((flg >> 5) & 1u) == 0;
+    f.block_sum = ((flg >> 4) & 1u) != 0;
+    f.content_sum = ((flg >> 2) & 1u) != 0;
+    if ((flg >> 3) & 1u) f.content = le64(in + 6);
+    return f;
+}
+
+// compute_frame_uncompressed_size (lz4_frame_compressor.cc:160-166): the
+// wrapper's first output chunk; only its header peek (src >= 19 bytes,
+// :189-200) sees contentSize
+RPC_HD uint64_t lz4_first_chunk(const Lz4Frame& f, uint64_t n) {
+    const uint64_t fs = n >= kLz4HeaderSizeMax ? f.content : 0;
+    const uint64_t w = (fs == 0 || fs > n * 255) ? n * 4 : fs;
+    return w < kMaxChunk ? w : kMaxChunk;
+}
+// End of the wrapper's output chunk that receives output byte s: chunks are
+// first, 2*first, ... capped at 128 KiB; a full chunk is flushed before the
+// next byte is produced.
+RPC_HD uint64_t lz4_chunk_end(uint64_t first, uint64_t s) {
+    uint64_t start = 0, c = first;
+    while (s >= start + c) {
+        start += c;
+        c = c * 2 < kMaxChunk ? c * 2 : kMaxChunk;
+    }
+    return start + c;
+}
+
+// lz4_frame_compressor::uncompress (lz4_frame_compressor.cc:168-278) for a
+// contiguous input of n > 0 bytes.  The wrapper stops at the first frame end
+// (LZ4F_decompress returns 0; unconsumed input -> LZ4_TRAILING) or when the
+// input runs out (truncated frame -> the output so far, no error).  The one
+// place its output chunking shows: a compressed block that ends exactly at
+// the end of the input and was decoded into LZ4F's tmpOut (less than
+// maxBlockSize of room left in the chunk) is flushed only as far as the
+// chunk has room, and the rest is dropped when the loop exits.
+RPC_HD int32_t lz4f_uncompress(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len) {
+    *out_len = 0;
+    const Lz4Frame f = lz4f_header(in, n);
+    if (f.kind == kLz4Error) return V_ERROR;
+    if (f.kind == kLz4Partial) return V_OK;  // header still incomplete when the input ran out
+    if (f.kind == kLz4Skip) {                 // skippable frame: 4-byte magic, LE32 size, payload
+        if (n < 8) return V_OK;
+        return (uint64_t)le32(in + 4) < n - 8 ? V_TRAILING : V_OK;
+    }
+    const uint64_t first = lz4_first_chunk(f, n);
+    uint64_t pos = f.hlen, o = 0;
+    for (;;) {
+        if (n - pos < 4) break;  // block header incomplete
+        const uint32_t bh = le32(in + pos);
+        pos += 4;
+        if (bh == 0) {  // end mark: dstage_getSuffix
+            if (f.content != 0 && o != f.content) return V_ERROR;  // frameSize_wrong
+            if (f.content_sum) {
+                if (n - pos < 4) break;
+                if (le32(in + pos) != xxh32(out, o, 0)) return V_ERROR;  // contentChecksum_invalid
+                pos += 4;
+            }
+            *out_len = o;
+            return pos < n ? V_TRAILING : V_OK;
+        }
+        const uint64_t size = bh & 0x7FFFFFFFu;
+        if (size > f.max_block) return V_ERROR;  // maxBlockSize_invalid
+        if (bh & 0x80000000u) {                  // uncompressed block: dstage_copyDirect
+            const uint64_t take = size < n - pos ? size : n - pos;
+            if (o + take > cap) {
+                *out_len = o;
+                return V_OVERFLOW;
+            }
+            copy_fwd(out + o, in + pos, take);
+            o += take;
+            pos += take;
+            if (take < size) break;
+            if (f.block_sum) {
+                if (n - pos < 4) break;
+                if (le32(in + pos) != xxh32(in + pos - size, size, 0)) return V_ERROR;
+                pos += 4;
+            }
+            continue;
+        }
+        const uint64_t need = size + (f.block_sum ? 4 : 0);
+        if (n - pos < need) break;  // block still being stored when the input ran out
+        if (f.block_sum && le32(in + pos + size) != xxh32(in + pos, size, 0)) return V_ERROR;
+        if (o + f.max_block > cap) {
+            *out_len = o;
+            return V_OVERFLOW;
+        }
+        const int64_t d = lz4_block(in + pos, (int64_t)size, out + o, f.max_block, f.linked ? (int64_t)o : 0);
+        if (d < 0) return V_ERROR;  // decompressionFailed
+        const uint64_t s = o;
+        o += (uint64_t)d;
+        pos += need;
+        if (pos == n) {
+            const uint64_t room = lz4_chunk_end(first, s) - s;
+            if (room < f.max_block && room < (uint64_t)d) o = s + room;
+            break;
+        }
+    }
+    *out_len = o;
+    return V_OK;
+}
+
+// Upper bound of lz4f_uncompress's output for any input: the partial copies
+// of uncompressed blocks plus maxBlockSize per complete compressed block.
+RPC_HD uint64_t lz4f_bound(const uint8_t* in, uint64_t n) {
+    const Lz4Frame f = lz4f_header(in, n);
+    if (f.kind != kLz4Frame) return 0;
+    uint64_t pos = f.hlen, b = 0;
+    while (n - pos >= 4) {
+        const uint32_t bh = le32(in + pos);
+        pos += 4;
+        if (bh == 0) break;
+        const uint64_t size = bh & 0x7FFFFFFFu;
+        if (size > f.max_block) break;
+        if (bh & 0x80000000u) {
+            const uint64_t take = size < n - pos ? size : n - pos;
+            b += take;
+            pos += take;
+            if (take < size) break;
+            if (f.block_sum) {
+                if (n - pos < 4) break;
+                pos += 4;
+            }
+        } else {
+            const uint64_t need = size + (f.block_sum ? 4 : 0);
+            if (n - pos < need) break;
+            b += f.max_block;
+            pos += need;
+        }
+    }
+    return b;
+}
+
+// ---------------------------------------------------------------- snappy
+// Varint::Parse32WithLimit (snappy 1.1.8): at most 5 bytes, the 5th < 16.
+RPC_HD bool snappy_varint(const uint8_t* p, uint64_t n, uint32_t& v, uint32_t& used) {
+    uint32_t r = 0;
+    for (uint32_t i = 0; i < 5; i++) {
+        if (i >= n) return false;
+        const uint32_t b = p[i];
+        r |= (b & 127u) << (7 * i);
+        if (i < 4 ? b < 128u : b < 16u) {
+            v = r;
+            used = i + 1;
+            return true;
+        }
+    }
+    return false;
+}
+
+// snappy::RawUncompress over one flat buffer: SnappyDecompressor::
+// DecompressAllTags into a SnappyArrayWriter of `expected` bytes.  A tag
+// needs its extra bytes present (RefillTag), a literal must fit the input
+// and the output, a copy must satisfy 0 < offset <= produced and fit the
+// output; success = the input ends at a tag boundary with exactly
+// `expected` bytes produced.
+RPC_HD bool snappy_raw(const uint8_t* in, uint64_t n, uint8_t* out, uint32_t expected, uint32_t hdr) {
+    uint64_t ip = hdr, op = 0;
+    for (;;) {
+        if (ip == n) return op == expected;  // eof at a tag boundary, CheckLength
+        const uint32_t c = in[ip];
+        const uint32_t type = c & 3u;
+        const uint32_t extra = type == 0 ? ((c >> 2) >= 60 ? (c >> 2) - 59 : 0) : (type == 3 ? 4 : type);
+        if (n - ip < extra + 1) return false;
+        ip++;
+        if (type == 0) {
+            uint32_t len = (c >> 2) + 1;
+            if (len >= 61) {
+                uint32_t v = 0;
+                for (uint32_t k = 0; k < extra; k++) v |= (uint32_t)in[ip + k] << (8 * k);
+                len = v + 1;  // uint32 arithmetic, as ExtractLowBytes(...) + 1
+                ip += extra;
+            }
+            if (n - ip < len) return false;        // premature end of input
+            if (op + len > expected) return false;  // SnappyArrayWriter::Append
+            copy_fwd(out + op, in + ip, len);
+            op += len;
+            ip += len;
+        } else {
+            uint32_t len, off;
+            if (type == 1) {
+                len = 4 + ((c >> 2) & 7u);
+                off = ((c >> 5) << 8) | in[ip];
+            } else if (type == 2) {
+                len = (c >> 2) + 1;
+                off = le16(in + ip);
+            } else {
+                len = (c >> 2) + 1;
+                off = le32(in + ip);
+            }
+            ip += extra;
+            if (off == 0 || op < off) return false;  // Produced() <= offset - 1u
+            if (op + len > expected) return false;
+            copy_match(out + op, off, len);
+            op += len;
+        }
+    }
+}
+
+// snappy_standard_compressor::uncompress_append via the C API as the oracle
+// calls it (oracle/codec.c snappy_raw_append): the length preamble, then a
+// raw decode of exactly that many bytes.  zero_skip: a 0-length preamble
+// yields nothing without looking further (the unframed path, :152-160).
+RPC_HD int32_t snappy_raw_append(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t& o,
+                                 bool zero_skip) {
+    uint32_t ulen, used;
+    if (!snappy_varint(in, n, ulen, used)) return V_ERROR;
+    if (zero_skip && ulen == 0) return V_OK;
+    if (o + ulen > cap) return V_OVERFLOW;
+    if (!snappy_raw(in, n, out + o, ulen, used)) return V_ERROR;
+    o += ulen;
+    return V_OK;
+}
+
+RPC_HD bool snappy_java_magic(const uint8_t* x) {
+    return x[0] == 0x82 && x[1] == 'S' && x[2] == 'N' && x[3] == 'A' && x[4] == 'P' && x[5] == 'P' &&
+           x[6] == 'Y' && x[7] == 0;
+}
+
+// snappy_java_compressor::uncompress (snappy_java_compressor.cc:76-110):
+// < 16 bytes or no magic -> raw snappy of the whole buffer; else the LE
+// min_version check and {BE i32 length, raw chunk} until the input is used.
+RPC_HD int32_t snappy_java_uncompress(const uint8_t* x, uint64_t n, uint8_t* out, uint64_t cap,
+                                      uint64_t* out_len) {
+    uint64_t o = 0;
+    int32_t v = V_OK;
+    if (n < 16 || !snappy_java_magic(x)) {
+        v = snappy_raw_append(x, n, out, cap, o, true);
+        *out_len = o;
+        return v;
+    }
+    if ((int32_t)le32(x + 12) < 1) return V_ERROR;  // min_version < 1
+    uint64_t pos = 16;
+    while (pos != n) {
+        if (n - pos < 4) {  // consume_be_type: out_of_range
+            v = V_ERROR;
+            break;
+        }
+        const int32_t clen = (int32_t)be32(x + pos);
+        pos += 4;
+        // iobuf_copy truncates to int; a negative length makes the reference
+        // allocate ~4 GiB of fragments (allocation-dependent, oracle/codec.c)
+        if (clen < 0 || (uint32_t)clen > (64u << 20)) {
+            v = V_UNDEFINED;
+            break;
+        }
+        const uint64_t take = (uint64_t)clen < n - pos ? (uint64_t)clen : n - pos;  // short copy
+        v = snappy_raw_append(x + pos, take, out, cap, o, false);
+        if (v != V_OK) break;
+        pos += take;
+    }
+    *out_len = o;
+    return v;
+}
+
+// Upper bound (exact for valid input) of snappy_java_uncompress's output:
+// the sum of the chunks' length preambles.
+RPC_HD uint64_t snappy_java_bound(const uint8_t* x, uint64_t n) {
+    uint32_t u, used;
+    if (n < 16 || !snappy_java_magic(x)) return snappy_varint(x, n, u, used) ? u : 0;
+    if ((int32_t)le32(x + 12) < 1) return 0;
+    uint64_t pos = 16, b = 0;
+    while (pos != n) {
+        if (n - pos < 4) break;
+        const int32_t clen = (int32_t)be32(x + pos);
+        pos += 4;
+        if (clen < 0 || (uint32_t)clen > (64u << 20)) break;
+        const uint64_t take = (uint64_t)clen < n - pos ? (uint64_t)clen : n - pos;
+        if (!snappy_varint(x + pos, take, u, used)) break;
+        b += u;
+        pos += take;
+    }
+    return b;
+}
+
+// ---------------------------------------------------------------- dispatch
+// compression::compressor::uncompress (compression.cc:35-55).  gzip (1) and
+// zstd (4) are not decoded by this engine yet: RPGPU_V_DECOMP_UNSUPPORTED.
+RPC_HD int32_t uncompress(uint32_t codec, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap,
+                          uint64_t* out_len) {
+    *out_len = 0;
+    if (n == 0) return V_ERROR;  // "Asked to decompress an empty buffer"
+    switch (codec) {
+    case 2: return snappy_java_uncompress(in, n, out, cap, out_len);
+    case 3: return lz4f_uncompress(in, n, out, cap, out_len);
+    case 1:
+    case 4: return V_UNSUPPORTED;
+    default: return V_ERROR;  // none: "nothing to uncompress"
+    }
+}
+
+RPC_HD uint64_t uncompress_bound(uint32_t codec, const uint8_t* in, uint64_t n) {
+    if (n == 0) return 0;
+    switch (codec) {
+    case 2: return snappy_java_bound(in, n);
+    case 3: return lz4f_bound(in, n);
+    default: return 0;
+    }
+}
+
+}  // namespace rpcodec
+#endif

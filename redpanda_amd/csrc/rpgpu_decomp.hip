@@ -1,0 +1,253 @@
+// rpgpu_decomp.hip — decompression of compressed record batches on the GPU.
+//
+// Replaces, per batch, compression::compressor::uncompress
+// (compression/compression.cc:35-55 and the codec wrappers restated in
+// rpgpu_codec.h) and the rewrite of storage::internal::
+// maybe_decompress_batch_sync (storage/parser_utils.cc:52-68,122-128): the
+// decompressed body becomes a new on-disk batch with the codec bits removed,
+// size_bytes = 61 + body, crc = crc_record_batch over the decompressed body
+// and header_crc = internal_header_only_crc, whose records are then walked
+// and indexed like those of any other batch.
+//
+// After validation of the compressed arena (validate_kernel):
+//   decomp_caps_kernel   one thread per batch: the batch's output slot =
+//                        61-byte header + an upper bound of the decoded size
+//                        read off the frame's block headers / chunk
+//                        preambles + kSlack; exclusive scan of the slots
+//   decomp_kernel        one lane per batch decodes its body into its slot
+//                        and writes the rewritten header (CRC fields 0) and
+//                        the rewritten batch's descriptor
+//   validate_kernel      over the rewritten batches with RPGPU_OP_RECRC: the
+//                        Kafka CRC of the decompressed body, then the header
+//                        CRC over the header carrying it; record walk; index
+//   decomp_patch_kernel  stores both CRCs into the rewritten headers
+// Decoding is one lane per batch: an LZ4 or snappy stream is a chain of
+// dependent sequences, and with every batch of an arena in flight at once
+// (C3: 262,144 lanes, 16 waves per CU) the chip is filled with batches
+// rather than by splitting one stream.
+#include "rpgpu_device.h"  // before rpgpu_codec.h: HIP attributes
+#include "rpgpu_codec.h"
+
+namespace rpgpu {
+
+hipError_t launch_block_scan(uint64_t* block_sum, uint32_t nb, uint64_t* total, hipStream_t s);
+hipError_t launch_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
+                       uint64_t* d_index_used, void* d_scratch, hipStream_t s);
+hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
+                      rpgpu_batch_result* d_res, rpgpu_record_index* d_index, uint64_t index_cap,
+                      const void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s);
+size_t validate_scratch_bytes(uint32_t n);
+
+namespace {
+// scratch: slot[n] u64 | local[n] u64 | block_sum[nb] u64 | validate scratch
+struct Parts {
+    uint64_t *slot, *local, *block_sum;
+    void* vscratch;
+};
+size_t parts_head(uint32_t n) {
+    const size_t nb = (n + kScanBlock - 1) / kScanBlock;
+    return ((size_t)n * 16 + nb * 8 + 255) & ~(size_t)255;
+}
+Parts parts(void* p, uint32_t n) {
+    uint8_t* b = static_cast<uint8_t*>(p);
+    Parts s;
+    s.slot = reinterpret_cast<uint64_t*>(b);
+    s.local = s.slot + n;
+    s.block_sum = s.local + n;
+    s.vscratch = b + parts_head(n);
+    return s;
+}
+}  // namespace
+
+size_t decomp_scratch_bytes(uint32_t n) { return parts_head(n) + validate_scratch_bytes(n); }
+
+__device__ __forceinline__ bool decomp_wanted(const rpgpu_batch_desc& d, const rpgpu_batch_result& v) {
+    return (d.ops & RPGPU_OP_DECOMP) && v.verdict == RPGPU_V_OK && v.codec != 0;
+}
+
+// output slot per batch + exclusive scan within blocks of kScanBlock batches
+__global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
+    const rpgpu_batch_result* __restrict__ vres, uint64_t* __restrict__ slot, uint64_t* __restrict__ local,
+    uint64_t* __restrict__ block_sum) {
+    __shared__ uint64_t wsum[kScanBlock / 64];
+    const uint32_t i = blockIdx.x * kScanBlock + threadIdx.x;
+    uint64_t sz = 0;
+    if (i < n) {
+        const rpgpu_batch_desc d = descs[i];
+        const rpgpu_batch_result v = vres[i];
+        if (decomp_wanted(d, v) && (v.codec == 2 || v.codec == 3)) {
+            // verdict OK: kHeaderSize <= size_bytes <= descriptor length
+            const uint64_t body = (uint64_t)(uint32_t)v.size_bytes - kHeaderSize;
+            const uint64_t bound = rpcodec::uncompress_bound(v.codec, data + d.offset + kHeaderSize, body);
+            sz = (kHeaderSize + bound + rpcodec::kSlack + 15) & ~(uint64_t)15;
+        }
+    }
+    const uint32_t l = lane_id();
+    uint64_t x = sz;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+        const uint32_t lo = __shfl_up((uint32_t)x, s, 64), hi = __shfl_up((uint32_t)(x >> 32), s, 64);
+        if (l >= (uint32_t)s) x += ((uint64_t)hi << 32) | lo;
+    }
+    const uint32_t wv = threadIdx.x >> 6;
+    if (l == 63) wsum[wv] = x;
+    __syncthreads();
+    uint64_t wbase = 0;
+    for (uint32_t k = 0; k < wv; k++) wbase += wsum[k];
+    if (i < n) {
+        slot[i] = sz;
+        local[i] = wbase + x - sz;
+    }
+    if (threadIdx.x == kScanBlock - 1) {
+        uint64_t tot = 0;
+        for (uint32_t k = 0; k < kScanBlock / 64; k++) tot += wsum[k];
+        block_sum[blockIdx.x] = tot;
+    }
+}
+
+// header field of the input batch: big-endian on the wire, little-endian on disk
+__device__ __forceinline__ uint64_t hdr_field(const uint8_t* p, int off, int nb, bool be) {
+    uint64_t v = 0;
+    for (int k = 0; k < nb; k++) v = be ? (v << 8) | p[off + k] : v | ((uint64_t)p[off + k] << (8 * k));
+    return v;
+}
+__device__ __forceinline__ void put_le(uint8_t* o, int off, uint64_t v, int nb) {
+    for (int k = 0; k < nb; k++) o[off + k] = (uint8_t)(v >> (8 * k));
+}
+
+__global__ __launch_bounds__(256) void decomp_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
+    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
+    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
+    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
+    rpgpu_batch_desc* __restrict__ out_descs) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const rpgpu_batch_desc d = descs[i];
+    const rpgpu_batch_result v = vres[i];
+    const uint64_t off = block_base[i / kScanBlock] + local[i];
+    const uint64_t sz = slot[i];
+    int32_t verdict = RPGPU_V_SKIPPED;
+    uint64_t len = 0;
+    uint8_t ops = 0;
+    if (decomp_wanted(d, v)) {
+        if (sz == 0) {
+            verdict = RPGPU_V_DECOMP_UNSUPPORTED;  // gzip, zstd
+        } else if (off + sz > out_cap) {
+            verdict = RPGPU_V_DECOMP_OVERFLOW;  // caller's buffer smaller than the plan
+        } else {
+            const uint8_t* p = data + d.offset;
+            uint8_t* o = out + off;
+            verdict = rpcodec::uncompress(v.codec, p + kHeaderSize, (uint64_t)(uint32_t)v.size_bytes - kHeaderSize,
+                                          o + kHeaderSize, sz - kHeaderSize - rpcodec::kSlack, &len);
+            if (verdict == RPGPU_V_OK) {
+                // rewritten header in the on-disk layout (storage/parser.cc:40-80):
+                // codec bits removed, size_bytes = 61 + body (parser_utils.cc:61-64,124);
+                // crc / header_crc follow from the validation of the rewritten batch
+                const bool be = d.format == RPGPU_FMT_KAFKA_WIRE;
+                put_le(o, 0, 0, 4);
+                put_le(o, 4, kHeaderSize + len, 4);
+                put_le(o, 8, be ? hdr_field(p, 0, 8, true) : hdr_field(p, 8, 8, false), 8);
+                o[16] = be ? (uint8_t)1 : p[16];  // raft_data on produce
+                put_le(o, 17, 0, 4);
+                put_le(o, 21, hdr_field(p, 21, 2, be) & ~(uint64_t)7, 2);
+                put_le(o, 23, hdr_field(p, 23, 4, be), 4);
+                put_le(o, 27, hdr_field(p, 27, 8, be), 8);
+                put_le(o, 35, hdr_field(p, 35, 8, be), 8);
+                put_le(o, 43, hdr_field(p, 43, 8, be), 8);
+                put_le(o, 51, hdr_field(p, 51, 2, be), 2);
+                put_le(o, 53, hdr_field(p, 53, 4, be), 4);
+                put_le(o, 57, hdr_field(p, 57, 4, be), 4);
+                ops = RPGPU_OP_CRC | RPGPU_OP_HDRCRC | RPGPU_OP_RECRC | (d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX));
+            }
+        }
+    }
+    rpgpu_decomp_result r;
+    r.verdict = verdict;
+    r.codec = v.codec;
+    r.out_offset = off;
+    r.out_len = len;
+    r.out_cap = sz;
+    dres[i] = r;
+    rpgpu_batch_desc od;
+    od.offset = off;
+    od.length = ops ? (uint32_t)(kHeaderSize + len) : 0u;
+    od.partition = d.partition;
+    od.format = RPGPU_FMT_RP_DISK;
+    od.ops = ops;
+    od.flags = 0;
+    od.reserved = 0;
+    out_descs[i] = od;
+}
+
+// stores the CRCs the validation of the rewritten batches computed
+__global__ __launch_bounds__(256) void decomp_patch_kernel(const rpgpu_decomp_result* __restrict__ dres,
+                                                           const rpgpu_batch_result* __restrict__ vres2, uint32_t n,
+                                                           uint8_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || dres[i].verdict != RPGPU_V_OK) return;
+    uint8_t* o = out + dres[i].out_offset;
+    put_le(o, 0, vres2[i].header_crc, 4);
+    put_le(o, 17, vres2[i].crc, 4);
+}
+
+// scalar mirror (rpgpu_uncompress): one lane
+__global__ void uncompress_bound_kernel(uint32_t codec, const uint8_t* in, uint64_t n, uint64_t* res) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) res[0] = rpcodec::uncompress_bound(codec, in, n);
+}
+__global__ void uncompress_one_kernel(uint32_t codec, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap,
+                                      uint64_t* res) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        uint64_t len = 0;
+        res[1] = (uint64_t)(int64_t)rpcodec::uncompress(codec, in, n, out, cap, &len);
+        res[2] = len;
+    }
+}
+
+// ------------------------------------------------------------ launchers
+hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
+                              const rpgpu_batch_result* d_vres, uint64_t* d_out_bytes, void* d_scratch,
+                              hipStream_t s) {
+    if (n == 0) return d_out_bytes ? hipMemsetAsync(d_out_bytes, 0, sizeof(uint64_t), s) : hipSuccess;
+    const Parts p = parts(d_scratch, n);
+    const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
+    decomp_caps_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_block_scan(p.block_sum, nb, d_out_bytes, s);
+}
+
+hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
+                             const rpgpu_batch_result* d_vres, rpgpu_decomp_result* d_dres, uint8_t* d_out,
+                             uint64_t out_cap, rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_vres2,
+                             rpgpu_record_index* d_index, uint64_t index_cap, uint64_t* d_index_used,
+                             void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s) {
+    if (n == 0) return d_index_used ? hipMemsetAsync(d_index_used, 0, sizeof(uint64_t), s) : hipSuccess;
+    const Parts p = parts(d_scratch, n);
+    const uint32_t nblk = (n + 255) / 256;
+    decomp_kernel<<<nblk, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
+                                       out_cap, d_out_descs);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if ((e = launch_plan(d_out_descs, n, d_out, d_index_used, p.vscratch, s)) != hipSuccess) return e;
+    if ((e = launch_run(d_out_descs, n, d_out, d_vres2, d_index, index_cap, p.vscratch, d_tables, grid, s)) !=
+        hipSuccess)
+        return e;
+    decomp_patch_kernel<<<nblk, 256, 0, s>>>(d_dres, d_vres2, n, d_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_uncompress_bound(uint32_t codec, const uint8_t* d_in, uint64_t n, uint64_t* d_res,
+                                   hipStream_t s) {
+    uncompress_bound_kernel<<<1, 64, 0, s>>>(codec, d_in, n, d_res);
+    return hipGetLastError();
+}
+
+hipError_t launch_uncompress_one(uint32_t codec, const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint64_t cap,
+                                 uint64_t* d_res, hipStream_t s) {
+    uncompress_one_kernel<<<1, 64, 0, s>>>(codec, d_in, n, d_out, cap, d_res);
+    return hipGetLastError();
+}
+
+}  // namespace rpgpu

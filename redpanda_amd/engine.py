@@ -111,7 +111,87 @@ class Engine:
         if rc != abi.RPGPU_OK:
             raise EngineError(f"rpgpu_crc32c_ranges_device: {rc} {self.last_error()}")
 
+    # -- decompression (rpgpu_decomp_plan_device / rpgpu_decomp_run_device) -------------
+    @staticmethod
+    def decomp_scratch_bytes(n: int) -> int:
+        return int(abi.lib().rpgpu_decomp_scratch_bytes(n))
+
+    def decomp_plan_device(self, d_descs: int, n: int, d_data: int, d_results: int, d_out_bytes: int,
+                           d_scratch: int, stream: int = 0) -> None:
+        rc = self._lib.rpgpu_decomp_plan_device(self._ctx, d_descs, n, d_data, d_results, d_out_bytes,
+                                                d_scratch, stream or None)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_decomp_plan_device: {rc} {self.last_error()}")
+
+    def decomp_run_device(self, d_descs: int, n: int, d_data: int, d_results: int, d_dres: int,
+                          d_out: int, out_cap: int, d_out_descs: int, d_out_results: int, d_index: int,
+                          index_cap: int, d_used: int, d_scratch: int, stream: int = 0) -> None:
+        rc = self._lib.rpgpu_decomp_run_device(self._ctx, d_descs, n, d_data, d_results, d_dres, d_out,
+                                               out_cap, d_out_descs, d_out_results, d_index or None,
+                                               index_cap, d_used or None, d_scratch, stream or None)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_decomp_run_device: {rc} {self.last_error()}")
+
+    def decompress_arena(self, data: np.ndarray, descs: np.ndarray) -> dict:
+        """Validate a host arena, then decompress, rewrite and walk its compressed
+        batches through the device entry points (HBM buffers from torch).
+        Returns host copies: results (validation), dres, out (output buffer),
+        out_descs, out_results, index, used, out_bytes."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        descs = np.ascontiguousarray(descs, dtype=abi.DESC_DTYPE)
+        n = len(descs)
+        sh = torch.cuda.current_stream(dev).cuda_stream
+        m = max(n, 1)
+        d_data = torch.from_numpy(data.copy()).to(dev)
+        d_descs = torch.from_numpy(descs.view(np.uint8).copy()).to(dev)
+        d_res = torch.zeros(m * 64, dtype=torch.uint8, device=dev)
+        d_used = torch.zeros(2, dtype=torch.int64, device=dev)
+        d_vscr = torch.zeros(max(self.scratch_bytes(n), 1), dtype=torch.uint8, device=dev)
+        self.validate_device(d_descs.data_ptr(), n, d_data.data_ptr(), d_res.data_ptr(), 0, 0,
+                             d_used.data_ptr(), d_vscr.data_ptr(), sh)
+        d_scr = torch.zeros(max(self.decomp_scratch_bytes(n), 1), dtype=torch.uint8, device=dev)
+        self.decomp_plan_device(d_descs.data_ptr(), n, d_data.data_ptr(), d_res.data_ptr(),
+                                d_used.data_ptr(), d_scr.data_ptr(), sh)
+        torch.cuda.synchronize(dev)
+        out_bytes = int(d_used[0].item())
+        results = d_res.cpu().numpy().view(abi.RESULT_DTYPE)[:n].copy()
+        out_cap = out_bytes + abi.ARENA_TAIL_PAD
+        index_cap = int(np.maximum(results["record_count"], 0).astype(np.int64).sum()) + 1
+        d_out = torch.zeros(out_cap, dtype=torch.uint8, device=dev)
+        d_dres = torch.zeros(m * 32, dtype=torch.uint8, device=dev)
+        d_odescs = torch.zeros(m * 24, dtype=torch.uint8, device=dev)
+        d_ores = torch.zeros(m * 64, dtype=torch.uint8, device=dev)
+        d_index = torch.zeros(index_cap * 32, dtype=torch.uint8, device=dev)
+        self.decomp_run_device(d_descs.data_ptr(), n, d_data.data_ptr(), d_res.data_ptr(),
+                               d_dres.data_ptr(), d_out.data_ptr(), out_cap, d_odescs.data_ptr(),
+                               d_ores.data_ptr(), d_index.data_ptr(), index_cap,
+                               d_used.data_ptr() + 8, d_scr.data_ptr(), sh)
+        torch.cuda.synchronize(dev)
+        used = int(d_used[1].item())
+        return dict(
+            results=results,
+            dres=d_dres.cpu().numpy().view(abi.DECOMP_RESULT_DTYPE)[:n].copy(),
+            out=d_out.cpu().numpy(),
+            out_descs=d_odescs.cpu().numpy().view(abi.DESC_DTYPE)[:n].copy(),
+            out_results=d_ores.cpu().numpy().view(abi.RESULT_DTYPE)[:n].copy(),
+            index=d_index.cpu().numpy().view(abi.INDEX_DTYPE)[: min(used, index_cap)].copy(),
+            used=used, out_bytes=out_bytes)
+
     # -- synchronous scalar mirrors ---------------------------------------------------
+    def uncompress(self, codec: int, data: bytes | np.ndarray, cap: int | None = None) -> tuple[int, bytes]:
+        """compression::compressor::uncompress on the GPU: (verdict, bytes)."""
+        a = np.ascontiguousarray(np.frombuffer(bytes(data), dtype=np.uint8))
+        cap = cap if cap is not None else max(1 << 16, a.size * 300)
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
+        n = C.c_size_t()
+        v = self._lib.rpgpu_uncompress(self._ctx, codec, a.ctypes.data if a.size else None, a.size,
+                                       out.ctypes.data, cap, C.byref(n))
+        if v < 0:
+            raise EngineError(f"rpgpu_uncompress: {v} {self.last_error()}")
+        return int(v), out[: min(n.value, cap)].tobytes()
     def crc32c_extend(self, crc: int, data: bytes | np.ndarray) -> int:
         buf = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
         buf = np.ascontiguousarray(buf, dtype=np.uint8)

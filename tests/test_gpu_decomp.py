@@ -1,0 +1,157 @@
+"""GPU parity of the decompress path (rpgpu_decomp_plan_device /
+rpgpu_decomp_run_device and the rpgpu_uncompress scalar mirror) against the
+oracle: compression::compressor::uncompress (compression/compression.cc:35-55)
+over liblz4 / snappy through the reference's wrapper loops, the batch rewrite
+of maybe_decompress_batch_sync (storage/parser_utils.cc:52-68,122-128) and the
+record walk of the rewritten batches.  Compared per batch: decompress verdict,
+decoded length, the rewritten batch's bytes (header with fresh CRCs + body),
+its validation result and its index entries.  zstd batches must report
+RPGPU_V_DECOMP_UNSUPPORTED (not decoded on the GPU yet)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.dirname(__file__))
+from kafka_batches import DISK, WIRE, arena, batch, record  # noqa: E402
+
+import oracle.oracle as orc  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+OPS = 1 | 2 | 4 | 8 | 16  # CRC | HDRCRC | PARSE | INDEX | DECOMP
+
+
+def compare(got, data, descs):
+    from redpanda_amd import abi
+
+    res, dres = got["results"], got["dres"]
+    wres, _, _ = orc.validate_arena(data, descs)
+    assert np.array_equal(res.view(np.uint8), wres.view(np.uint8)), "validation results differ"
+    caps = np.where(dres["out_cap"] > 0, dres["out_cap"].astype(np.int64) - 61 - 128, 0).astype(np.uint64)
+    want = orc.decompress_arena(data, descs, wres, caps)
+    bad = np.nonzero(dres["verdict"] != want["verdicts"])[0]
+    assert bad.size == 0, (f"decompress verdicts differ at {bad[:8]}: gpu {dres['verdict'][bad[:8]]} "
+                           f"oracle {want['verdicts'][bad[:8]]}")
+    ok = np.nonzero(dres["verdict"] == abi.V_OK)[0]
+    assert np.array_equal(dres["out_len"][ok], want["out_len"][ok]), "decoded lengths differ"
+    for i in ok:
+        a = int(dres["out_offset"][i])
+        b = int(want["out_descs"]["offset"][i])
+        m = 61 + int(dres["out_len"][i])
+        assert np.array_equal(got["out"][a:a + m], want["out"][b:b + m]), f"rewritten batch {i} differs"
+    ores, wores = got["out_results"], want["out_results"]
+    for f in abi.RESULT_DTYPE.names:
+        bad = np.nonzero(ores[f] != wores[f])[0]
+        assert bad.size == 0, f"rewritten-batch field {f} differs at {bad[:8]}: {ores[f][bad[:8]]} vs {wores[f][bad[:8]]}"
+    assert got["used"] == want["used"]
+    assert np.array_equal(got["index"].view(np.uint8), want["index"].view(np.uint8)), "index differs"
+    return want
+
+
+def records(rng, n, key_len, value_len, text):
+    out = []
+    for j in range(n):
+        if text:
+            words = [b"kafka", b"redpanda", b"offset", b"batch", b"the", b"log", b"segment", b"x"]
+            v = b" ".join(words[k] for k in rng.integers(0, len(words), value_len // 5 + 1))[:value_len]
+        else:
+            v = bytes(rng.integers(97, 123, value_len, dtype=np.uint8))
+        k = bytes(rng.integers(65, 91, key_len, dtype=np.uint8)) if key_len >= 0 else None
+        out.append(record(k, v, ts_delta=j, off_delta=j,
+                          headers=[(b"h", b"v" * int(rng.integers(0, 5)))] if j % 3 == 0 else []))
+    return out
+
+
+@pytest.mark.parametrize("codec", [2, 3])
+@pytest.mark.parametrize("fmt", [WIRE, DISK])
+def test_generated_arenas(eng, codec, fmt):
+    """Builder arenas (rpgen: the reference's compressor settings), text and alnum payloads."""
+    from redpanda_amd import abi, engine
+
+    for payload, shape in ((abi.PAYLOAD_TEXT, (12, 8, 700)), (abi.PAYLOAD_ALNUM, (5, 16, 3000))):
+        spec = engine.make_spec(seed=0x5EED0003 + codec, partitions=4, records_per_batch=shape[0],
+                                key_len=shape[1], value_len=shape[2], codec=codec, format=fmt,
+                                ops=abi.OPS_PRODUCE | abi.OP_DECOMP, payload=payload)
+        data, descs = engine.build_arena(spec, 48)
+        got = eng.decompress_arena(data, descs)
+        compare(got, data, descs)
+        assert (got["dres"]["verdict"] == abi.V_OK).all()
+
+
+def test_mixed_codecs_corrupted(eng):
+    """C5-shaped arena: none/snappy/lz4/zstd, skewed sizes, 1-in-4 corrupted batches."""
+    from redpanda_amd import abi, engine
+
+    spec = engine.make_spec(seed=0x5EED0005, partitions=16, codec_mix=(1 << 0) | (1 << 2) | (1 << 3) | (1 << 4),
+                            body_min=7, body_max=300_000, ops=abi.OPS_PRODUCE | abi.OP_DECOMP,
+                            payload=abi.PAYLOAD_TEXT, corrupt_ppm=250_000, corrupt_mask=0x3FF)
+    data, descs = engine.build_arena(spec, 160)
+    got = eng.decompress_arena(data, descs)
+    compare(got, data, descs)
+    v = got["dres"]["verdict"]
+    assert (v == abi.V_DECOMP_UNSUPPORTED).sum() > 0  # zstd
+    assert (v == abi.V_OK).sum() > 10
+
+
+def mutated_bodies(rng, codec, n):
+    """Compressed bodies (whole-frame or chunk level) mutated the ways a bad
+    producer or a bit flip would: truncation anywhere / at LZ4 block ends,
+    flipped bytes, trailing junk, altered lengths; re-CRC'd by batch()."""
+    out = []
+    for i in range(n):
+        recs = records(rng, int(rng.integers(1, 40)), int(rng.integers(-1, 20)),
+                       int(rng.integers(0, 3000)), text=bool(i % 2))
+        body = b"".join(recs)
+        comp = bytearray(orc.compress(codec, body))
+        kind = i % 7
+        if kind == 1:
+            comp = comp[:int(rng.integers(0, len(comp) + 1))]
+        elif kind == 2 and len(comp) > 0:
+            for _ in range(int(rng.integers(1, 4))):
+                comp[int(rng.integers(0, len(comp)))] ^= int(rng.integers(1, 256))
+        elif kind == 3:
+            comp += bytes(rng.integers(0, 256, int(rng.integers(1, 9)), dtype=np.uint8))
+        elif kind == 4 and codec == 3 and len(comp) > 11:
+            comp = comp[:-4]  # no end mark: truncated right after the last block
+        elif kind == 5 and len(comp) > 20:
+            k = int(rng.integers(16, len(comp)))
+            comp[k] = 0xFF
+        out.append((bytes(comp), len(recs)))
+    return out
+
+
+@pytest.mark.parametrize("codec", [2, 3])
+@pytest.mark.parametrize("fmt", [WIRE, DISK])
+def test_mutated_payloads(eng, codec, fmt):
+    rng = np.random.default_rng(100 + codec * 2 + fmt)
+    bs = [batch(c, fmt=fmt, record_count=rc, attrs=codec) for c, rc in mutated_bodies(rng, codec, 70)]
+    data, descs = arena(bs, fmt=fmt, ops=OPS)
+    compare(eng.decompress_arena(data, descs), data, descs)
+
+
+def test_large_bodies(eng):
+    """~1 MiB bodies: many 64 KiB LZ4 blocks, several 128 KiB snappy-java chunks."""
+    rng = np.random.default_rng(7)
+    bs = []
+    for codec in (2, 3, 3, 2):
+        recs = records(rng, 900, 8, 1100, text=codec == 3)
+        bs.append(batch(orc.compress(codec, b"".join(recs)), fmt=WIRE, record_count=len(recs), attrs=codec))
+    data, descs = arena(bs, fmt=WIRE, ops=OPS)
+    compare(eng.decompress_arena(data, descs), data, descs)
+
+
+def test_uncompress_scalar_mirror(eng):
+    rng = np.random.default_rng(3)
+    cases = []
+    for codec in (2, 3):
+        for c, _ in mutated_bodies(rng, codec, 40):
+            cases.append((codec, c))
+    cases += [(3, b""), (2, b""), (0, b"abc"), (3, b"\x04\x22\x4d"), (2, b"\x00")]
+    for codec, c in cases:
+        gv, gout = eng.uncompress(codec, c, cap=1 << 21)
+        ov, oout = orc.uncompress(codec, c, cap=1 << 21)
+        assert gv == ov, (codec, len(c), gv, ov)
+        if ov == 0:
+            assert gout == oout, (codec, len(c))
