@@ -8,6 +8,12 @@ resident in HBM.  Workload (BASELINE.json configs[1], "C2"): 1,048,576
 uncompressed Kafka v2 batches of 16,381 B (16 records x (16 B key + 995 B
 value)) over 4096 partitions per GPU.
 
+--config c3 (BASELINE.json configs[2]): 262,144 LZ4-frame batches of 64
+records x 1 KiB per GPU; one step = validation of the compressed batches,
+LZ4F decompression, the batch rewrite with fresh CRCs
+(maybe_decompress_batch_sync) and the record walk + index of the
+decompressed records.
+
 Multi-GPU: one process per GPU (torch.distributed, RCCL).  Partitions shard
 across GPUs (each rank owns its own partition range, weak scaling); the only
 exchange is the final gather of the per-rank verdict histogram.
@@ -38,6 +44,13 @@ CONFIGS = {
                  "Kafka CRC32C + internal header CRC + record walk + offset/timestamp index",
         batches=1 << 20, partitions=4096,
         spec=dict(records_per_batch=16, key_len=16, value_len=995)),
+    "c3": dict(
+        workload="C3: 262,144 LZ4-frame Kafka v2 batches per GPU, 64 records x 1 KiB (~64 KiB "
+                 "uncompressed), 4096 partitions; CRC32C + header CRC of the compressed batch, "
+                 "LZ4F decompression, batch rewrite with fresh CRCs, record walk + index of the "
+                 "decompressed records",
+        batches=1 << 18, partitions=4096, decompress=True,
+        spec=dict(records_per_batch=64, key_len=16, value_len=999, codec=3)),
     "c1": dict(
         workload="C1: 10,000 uncompressed Kafka v2 batches x 16,445 B (16 x 1 KiB records), "
                  "1 partition; CRC32C + header CRC + parse",
@@ -60,6 +73,8 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--ops", type=int, default=0, help="override the rpgpu_op mask (diagnostics)")
+    ap.add_argument("--payload", default="text", choices=["text", "alnum"],
+                    help="record payload of the compressed configs (text: Zipf words, alnum: random)")
     args = ap.parse_args()
 
     import torch
@@ -78,8 +93,11 @@ def main() -> int:
     cfg = CONFIGS[args.config]
     n = args.batches or cfg["batches"]
     P = cfg["partitions"]
-    spec = engine.make_spec(seed=0x5EED0000 + (2 if args.config == "c2" else 1), partitions=P,
-                            **cfg["spec"])
+    decompress = bool(cfg.get("decompress"))
+    spec = engine.make_spec(seed=0x5EED0000 + int(args.config[1:]), partitions=P, **cfg["spec"])
+    if decompress:
+        spec.ops = abi.OPS_PRODUCE | abi.OP_DECOMP
+        spec.payload = abi.PAYLOAD_TEXT if args.payload == "text" else abi.PAYLOAD_ALNUM
     if args.ops:
         spec.ops = args.ops
     eng = engine.Engine(local)
@@ -145,6 +163,27 @@ def main() -> int:
     d_index = torch.zeros(max(index_cap, 1) * 32, dtype=torch.uint8, device=dev)
     verdicts = d_res.view(torch.int32).view(n, 16)[:, 0]
     hist_sum = torch.zeros(64, dtype=torch.int64, device=dev)
+    if decompress:
+        # validate once, then plan the output (slot sizes depend only on the
+        # frames' block headers, so the buffers are sized once)
+        eng.run_device(d_descs.data_ptr(), n, data.data_ptr(), d_res.data_ptr(),
+                       d_index.data_ptr(), index_cap, d_scratch.data_ptr(), sh)
+        d_dscr = torch.zeros(engine.Engine.decomp_scratch_bytes(n), dtype=torch.uint8, device=dev)
+        d_obytes = torch.zeros(2, dtype=torch.int64, device=dev)
+        eng.decomp_plan_device(d_descs.data_ptr(), n, data.data_ptr(), d_res.data_ptr(),
+                               d_obytes.data_ptr(), d_dscr.data_ptr(), sh)
+        torch.cuda.synchronize()
+        out_cap = int(d_obytes[0].item()) + abi.ARENA_TAIL_PAD
+        rc_total = int(d_res.view(torch.int32).view(n, 16)[:, 5].clamp(min=0).sum().item())
+        d_out = torch.zeros(out_cap, dtype=torch.uint8, device=dev)
+        d_dres = torch.zeros(n * 32, dtype=torch.uint8, device=dev)
+        d_odescs = torch.zeros(n * 24, dtype=torch.uint8, device=dev)
+        d_ores = torch.zeros(n * 64, dtype=torch.uint8, device=dev)
+        d_index2 = torch.zeros(max(rc_total, 1) * 32, dtype=torch.uint8, device=dev)
+        dverdicts = d_dres.view(torch.int32).view(n, 8)[:, 0]
+        overdicts = d_ores.view(torch.int32).view(n, 16)[:, 0]
+        log(f"[rank {rank}] decompress plan: {out_cap / 2**30:.2f} GiB of output slots, "
+            f"{rc_total} records")
 
     run_events = []
 
@@ -157,11 +196,21 @@ def main() -> int:
             e0.record(stream)
         eng.run_device(d_descs.data_ptr(), n, data.data_ptr(), d_res.data_ptr(),
                        d_index.data_ptr(), index_cap, d_scratch.data_ptr(), sh)
+        if decompress:
+            eng.decomp_plan_device(d_descs.data_ptr(), n, data.data_ptr(), d_res.data_ptr(),
+                                   d_obytes.data_ptr(), d_dscr.data_ptr(), sh)
+            eng.decomp_run_device(d_descs.data_ptr(), n, data.data_ptr(), d_res.data_ptr(),
+                                  d_dres.data_ptr(), d_out.data_ptr(), out_cap, d_odescs.data_ptr(),
+                                  d_ores.data_ptr(), d_index2.data_ptr(), max(rc_total, 1),
+                                  d_obytes.data_ptr() + 8, d_dscr.data_ptr(), sh)
         if timed:
             e1.record(stream)
             run_events.append((e0, e1))
-        # final gather of per-rank results: the verdict histogram
+        # final gather of per-rank results: the verdict histogram (for the
+        # decompress configs: of the decompression and of the rewritten batches)
         hist = torch.bincount(verdicts, minlength=64)
+        if decompress:
+            hist = hist + torch.bincount(dverdicts, minlength=64) + torch.bincount(overdicts, minlength=64)
         if world > 1:
             dist.all_reduce(hist)
         hist_sum.copy_(hist)
@@ -187,10 +236,22 @@ def main() -> int:
     # ---- correctness of the timed output ------------------------------------------
     res = d_res.cpu().numpy().view(abi.RESULT_DTYPE)
     hist = hist_sum.cpu().numpy()
-    ok_all = int(hist[abi.V_OK]) == n * world
     wire = float(descs["length"].astype(np.float64).sum())
-    idx_entries = int(res["index_count"].astype(np.int64).sum())
-    alg_bytes = wire + 64.0 * n + 32.0 * idx_entries  # A = W + D + I
+    if decompress:
+        dres = d_dres.cpu().numpy().view(abi.DECOMP_RESULT_DTYPE)
+        ores = d_ores.cpu().numpy().view(abi.RESULT_DTYPE)
+        ok_all = int(hist[abi.V_OK]) == 3 * n * world
+        dec = float(dres["out_len"].astype(np.float64).sum())
+        idx_entries = int(ores["index_count"].astype(np.int64).sum())
+        # A = W + D + I; I = validation result + decompress
+        # result + rewritten header and result + 32 B per indexed record
+        alg_bytes = wire + dec + (64.0 + 32.0 + 61.0 + 64.0) * n + 32.0 * idx_entries
+        logical = 61.0 * n + dec
+    else:
+        ok_all = int(hist[abi.V_OK]) == n * world
+        idx_entries = int(res["index_count"].astype(np.int64).sum())
+        alg_bytes = wire + 64.0 * n + 32.0 * idx_entries  # A = W + D + I
+        logical = wire
 
     ms_per_step = elapsed / args.steps * 1e3
     value = wire * world * args.steps / elapsed / 1e9
@@ -205,12 +266,16 @@ def main() -> int:
                    "batch_bytes": int(descs["length"][0]), "partitions_per_gpu": P,
                    "parallelism": f"partition-shard x{world}"},
         "per_gpu_gbps": round(value / world, 2),
+        "logical_gbps": round(logical * world * args.steps / elapsed / 1e9, 2),
         "algorithmic_gbps_per_gpu": round(alg_bytes * args.steps / elapsed / 1e9, 2),
         "all_verdicts_ok": ok_all,
         "h2d_gbps_pinned": round(h2d_bytes / h2d_time / 1e9, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": None, "kernel": "validate_kernel",
+                     "traffic": None,
+                     "kernel": ("pipeline: validate_kernel + decomp_caps/decomp_kernel + "
+                                "validate_kernel over the rewritten batches" if decompress
+                                else "validate_kernel"),
                      "kernel_ms": round(run_ms, 4),
                      "algorithmic_bytes_per_launch": int(alg_bytes)},
         "cpu_baseline": None,
@@ -233,7 +298,43 @@ def main() -> int:
             pass
 
     # ---- CPU baseline: the oracle (C restatement, SSE4.2 CRC) on host cores --------
-    if rank == 0 and not args.no_cpu_baseline:
+    if decompress:
+        out["config"]["payload"] = args.payload
+        out["config"]["compressed_bytes_per_batch_avg"] = round(wire / n, 1)
+        out["config"]["decompressed_bytes_per_batch_avg"] = round(dec / n, 1)
+    if rank == 0 and not args.no_cpu_baseline and decompress:
+        import oracle.oracle as orc
+
+        T = args.cpu_threads or nthreads
+        sample_n = min(n, 2048)
+        sdata, sdescs = engine.build_arena(spec, sample_n, first=first, nthreads=nthreads)
+        sw = float(sdescs["length"].astype(np.float64).sum())
+        caps = np.full(sample_n, 256 << 10, dtype=np.uint64)  # ~64 KiB decompressed per batch
+
+        def cpu_pass():
+            r0, _, _ = orc.validate_arena(sdata, sdescs, nthreads=T, fast_crc=True)
+            return r0, orc.decompress_arena(sdata, sdescs, r0, caps, nthreads=T)
+
+        cpu_pass()  # warm-up
+        times, passes = [], 0
+        t_start = time.perf_counter()
+        while passes < 3 or (time.perf_counter() - t_start < 10.0 and passes < 30):
+            t1 = time.perf_counter()
+            r0, want = cpu_pass()
+            times.append(time.perf_counter() - t1)
+            passes += 1
+        cpu_gbps = sw / float(np.median(times)) / 1e9
+        same = (np.array_equal(dres["verdict"][:sample_n], want["verdicts"])
+                and np.array_equal(dres["out_len"][:sample_n], want["out_len"])
+                and all(np.array_equal(ores[f][:sample_n], want["out_results"][f])
+                        for f in abi.RESULT_DTYPE.names if f != "index_first"))
+        out["cpu_baseline"] = {
+            "value": round(cpu_gbps, 2), "unit": "GB/s", "cores": T, "kind": "port",
+            "sample": f"first {sample_n} batches of this workload ({sw / 1e9:.3f} GB compressed), "
+                      f"median of {passes} passes: oracle/ C restatement (SSE4.2 CRC32C) + the "
+                      f"reference's LZ4F wrapper loop over liblz4 1.9.3 + rewrite + walk"}
+        out["gpu_matches_oracle_on_sample"] = bool(same)
+    elif rank == 0 and not args.no_cpu_baseline:
         import oracle.oracle as orc
 
         T = args.cpu_threads or nthreads

@@ -121,6 +121,16 @@ def lib() -> C.CDLL:
         if not path.exists():
             raise RuntimeError(f"{path} is missing: run __graft_entry__.build() "
                                "(the engine has no CPU fallback)")
+        # One HIP runtime per process: torch bundles its own libamdhip64
+        # (SONAME libamdhip64.so.7) and needs it as "libamdhip64.so".  Loaded
+        # first, it also satisfies librpgpu.so's libamdhip64.so.7; loaded
+        # second, it would bring up a second HIP/HSA runtime that cannot open
+        # the device.  So torch (device buffers in bench.py and the tests) is
+        # imported before the engine library whenever it is installed.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(str(path))
         _sig(L.rpgpu_abi_version, _i32)
         _sig(L.rpgpu_open, _vp, C.c_int, _vp)
@@ -141,6 +151,9 @@ def lib() -> C.CDLL:
         _sig(L.rpgpu_crc32c_extend, _u32, _vp, _u32, _vp, C.c_size_t)
         _sig(L.rpgpu_internal_header_only_crc, _u32, _vp, _vp)
         _sig(L.rpgpu_crc_record_batch, _i32, _vp, _vp, _vp, C.c_size_t)
+        if not hasattr(L, "rpgpu_decomp_scratch_bytes"):  # an older build (A/B timing runs)
+            _LIB = L
+            return _LIB
         _sig(L.rpgpu_decomp_scratch_bytes, C.c_size_t, _u32)
         _sig(L.rpgpu_decomp_plan_device, _i32, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp)
         _sig(L.rpgpu_decomp_run_device, _i32, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp,

@@ -29,23 +29,10 @@ constexpr int kOffHB = kOffU + kRowsPerChunk * 128;
 constexpr int kTableWords = kOffHB + 2 * 16 * 64;
 static_assert(kTableWords % 4 == 0, "table blob is copied as 16-byte words");
 
-// validate_kernel workgroup: kCrcWaves checksum waves + 1 record-walk wave
-#ifndef RPGPU_CRC_WAVES
-#define RPGPU_CRC_WAVES 4
-#endif
-constexpr int kCrcWaves = RPGPU_CRC_WAVES;
-constexpr int kValidateThreads = (kCrcWaves + 1) * 64;
-// register budget of validate_kernel: waves per SIMD it must fit
-// (kBlocksPerCU workgroups of kCrcWaves + 1 waves on 4 SIMDs)
-#ifndef RPGPU_VALIDATE_WPE
-#define RPGPU_VALIDATE_WPE 5
-#endif
-constexpr int kValidateWavesPerEU = RPGPU_VALIDATE_WPE;
-constexpr int kRing = 64;  // walk jobs queued per workgroup (LDS ring)
-// crc_ranges_kernel workgroup
-constexpr int kRangesThreads = 256;
-constexpr int kWavesPerBlock = kRangesThreads / 64;
-constexpr int kBlocksPerCU = 4;  // default grid: workgroups per CU
+constexpr int kValidateThreads = 256;  // 4 waves per workgroup
+constexpr int kWavesPerBlock = kValidateThreads / 64;
+constexpr int kBlocksPerCU = 4;        // default grid: 16 waves per CU
+constexpr int kGroup = 64;             // batches per wave between record walks (one per lane)
 constexpr int kScanBlock = 1024;
 
 void build_tables(uint32_t* out /* kTableWords */);

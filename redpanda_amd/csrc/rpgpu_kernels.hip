@@ -22,9 +22,7 @@
 // batch's) rows are loaded into the registers each row frees as it is
 // checksummed, so 8 KiB per wave stay in flight.
 //
-// (2) Record walk (rpgpu_walk.h): every batch that needs one becomes a job
-// in the workgroup's LDS ring; the workgroup's walker wave walks up to 64
-// jobs at a time, one lane per batch, while the checksum waves stream on.
+// (2) Record walk (rpgpu_walk.h), one lane per batch of the group.
 //
 // RPGPU_OP_RECRC (the rewritten batches of rpgpu_decomp_run_device): the
 // header CRC is not checked but computed after the Kafka CRC, over a header
@@ -82,9 +80,7 @@ struct Result {
 // keeps the SLP vectorizer from turning the field reads into vector loads of
 // the struct, which would force the struct into scratch memory.
 __device__ __forceinline__ uint32_t u32s(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-// all = false: the batch was handed to the walker, which owns dword 0
-// (verdict) and dword 15 (index_count).
-__device__ __forceinline__ void write_result(rpgpu_batch_result* out, const Result& r, bool all) {
+__device__ __forceinline__ void write_result(rpgpu_batch_result* out, const Result& r) {
     if (lane_id() == 0) {
         const uint64_t bo = (uint64_t)r.h.base_offset, ft = (uint64_t)r.h.first_ts, mt = (uint64_t)r.h.max_ts;
         u32x4 a = {u32s((uint32_t)r.verdict), u32s(r.crc), u32s(r.crc_expected), u32s(r.header_crc)};
@@ -96,20 +92,10 @@ __device__ __forceinline__ void write_result(rpgpu_batch_result* out, const Resu
                    u32s((uint32_t)ft), u32s((uint32_t)(ft >> 32))};
         u32x4 d = {u32s((uint32_t)mt), u32s((uint32_t)(mt >> 32)), u32s(r.index_first), u32s(r.index_count)};
         u32x4* o = reinterpret_cast<u32x4*>(out);
+        o[0] = a;
         o[1] = b;
         o[2] = c;
-        if (all) {
-            o[0] = a;
-            o[3] = d;
-        } else {
-            uint32_t* w = reinterpret_cast<uint32_t*>(out);
-            w[1] = a.y;
-            w[2] = a.z;
-            w[3] = a.w;
-            w[12] = d.x;
-            w[13] = d.y;
-            w[14] = d.z;
-        }
+        o[3] = d;
     }
 }
 
@@ -233,12 +219,12 @@ __device__ __forceinline__ u32x4 merge_header(u32x4 y, int32_t ro0, uint32_t v_i
 
 // Checksums one batch whose header window and first rows are in `pf` and,
 // as the rows free their registers, loads the next batch's rows into them.
-// A batch that needs a record walk is pushed to the walker's ring.
+// A batch that needs a record walk becomes lane j's WalkJob.
 __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, const rpgpu_batch_desc& d,
                                               uint32_t b, const uint8_t* __restrict__ data,
                                               rpgpu_batch_result* __restrict__ res, uint32_t index_first,
                                               uint32_t cap, Prefetch& pf, const rpgpu_batch_desc& nd,
-                                              bool has_next, Ring* ring DIAG_PARAM) {
+                                              bool has_next, WalkJob& J, uint32_t j DIAG_PARAM) {
     const uint32_t l = lane_id();
     const uint8_t* p = data + d.offset;
     const uint32_t len = d.length;
@@ -370,7 +356,7 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
         // nothing of this batch is checksummed: just move the next one's rows
         load_rows(pf.x, nrs, ngm, 0, l);
         pf.gm = ngm;
-        write_result(res + b, r, true);
+        write_result(res + b, r);
         return;
     }
 
@@ -420,12 +406,6 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
             y.x ^= c;
             c = crc_block(sN, y);
             pf.x[k] = load_row(lrs, lg, lrow + k, l);
-            // keep the refill where it is: without this the scheduler sinks
-            // all eight loads to the end of the chunk, and the wave drains
-            // its rows in flight every chunk (ALU and LDS work of the next
-            // row may still move above it)
-            __builtin_amdgcn_sched_barrier(0x7CF);
-            asm volatile("" ::: "memory");
         }
     }
     pf.gm = ngm;
@@ -457,46 +437,37 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
     } else if (codec > 4) {
         r.verdict = RPGPU_V_BAD_CODEC_THROW;
     } else if (codec == 0 && (d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX))) {
-        // the walker writes the verdict and index_count
-        WalkJob J;
-        J.body = d.offset + kHeaderSize;
-        J.base_offset = r.h.base_offset;
-        J.first_ts = r.h.first_ts;
-        J.n = (uint32_t)(n - kHeaderSize);
-        J.rc = r.h.record_count;
-        J.first = index_first;
-        J.cap = cap;
-        J.b = b;
-        J.flags = kJobLive | ((d.ops & RPGPU_OP_INDEX) ? kJobIndex : 0u);
-        write_result(res + b, r, false);
-        ring_push(ring, J);
-        STAMP(3);
-        return;
+        // walked with the rest of the group; the walk patches verdict and
+        // index_count
+        if (l == j) {
+            J.body = d.offset + kHeaderSize;
+            J.base_offset = r.h.base_offset;
+            J.first_ts = r.h.first_ts;
+            J.n = (uint32_t)(n - kHeaderSize);
+            J.rc = r.h.record_count;
+            J.first = index_first;
+            J.cap = cap;
+            J.b = b;
+            J.flags = kJobLive | ((d.ops & RPGPU_OP_INDEX) ? kJobIndex : 0u);
+        }
     }
-    write_result(res + b, r, true);
+    write_result(res + b, r);
     STAMP(3);
 }
 
-// kCrcWaves checksum waves per workgroup, one batch per wave at a time,
-// grid-stride; the last wave of the workgroup walks records (rpgpu_walk.h).
-// index_first[i] = local exclusive prefix, block_base[i / kScanBlock] =
-// prefix of earlier scan blocks.
-__global__ __launch_bounds__(kValidateThreads) __attribute__((amdgpu_waves_per_eu(kValidateWavesPerEU, kValidateWavesPerEU))) void validate_kernel(
+// One wave per batch, grid-stride; every 64 batches of a wave are walked
+// together.  index_first[i] = local exclusive prefix, block_base[i /
+// kScanBlock] = prefix of earlier scan blocks.
+__global__ __launch_bounds__(kValidateThreads) void validate_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
     rpgpu_batch_result* __restrict__ res, rpgpu_record_index* __restrict__ index,
     const uint32_t* __restrict__ local_first, const uint32_t* __restrict__ caps,
     const uint64_t* __restrict__ block_base, uint64_t index_cap, const uint32_t* __restrict__ tables) {
     __shared__ __attribute__((aligned(16))) uint32_t sT[kTableWords];
-    __shared__ Ring ring;
-    ring_init(&ring);
     load_tables(sT, tables);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (wave == (uint32_t)kCrcWaves) {
-        walker(&ring, data, index, res, kCrcWaves);
-        return;
-    }
-    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kCrcWaves + wave);
-    const uint32_t nw = gridDim.x * kCrcWaves;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + wave);
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
 #ifdef RPGPU_DIAG_STAMPS
     Stamps sp{};
     sp.prev = __builtin_amdgcn_s_memtime();
@@ -511,22 +482,34 @@ __global__ __launch_bounds__(kValidateThreads) __attribute__((amdgpu_waves_per_e
         pf.gm = desc_geometry(d0);
         load_rows(pf.x, rs0, pf.gm, 0, lane_id());
     }
-    for (uint32_t b = gw; b < n; b += nw) {
-        const rpgpu_batch_desc d = sload_desc(descs + b);
-        const bool has_next = b + nw < n;
-        // always loaded (the batch's own descriptor when there is no next
-        // one; has_next masks its use): a conditionally initialised struct
-        // is lowered to scratch memory
-        const rpgpu_batch_desc nd = sload_desc(descs + (has_next ? b + nw : b));
-        const uint64_t first = sload(block_base + b / kScanBlock) + sload(local_first + b);
-        // never write past the caller's index buffer (rpgpu_validate_device)
-        uint64_t cap = sload(caps + b);
-        if (first >= index_cap) cap = 0;
-        else if (first + cap > index_cap) cap = index_cap - first;
-        process_batch(sT, d, b, data, res, (uint32_t)first, (uint32_t)cap, pf, nd, has_next, &ring DIAG_PASS);
+    for (uint32_t g = gw; g < n; g += kGroup * nw) {
+        WalkJob J;
+        J.flags = 0;
+        for (uint32_t j = 0; j < (uint32_t)kGroup; j++) {
+            const uint32_t b = g + j * nw;
+            if (b >= n) break;
+            const rpgpu_batch_desc d = sload_desc(descs + b);
+            const bool has_next = b + nw < n;
+            // always loaded (the batch's own descriptor when there is no
+            // next one; has_next masks its use): a conditionally initialised
+            // struct is lowered to scratch memory
+            const rpgpu_batch_desc nd = sload_desc(descs + (has_next ? b + nw : b));
+            const uint64_t first = sload(block_base + b / kScanBlock) + sload(local_first + b);
+            // never write past the caller's index buffer (rpgpu_validate_device)
+            uint64_t cap = sload(caps + b);
+            if (first >= index_cap) cap = 0;
+            else if (first + cap > index_cap) cap = index_cap - first;
+            process_batch(sT, d, b, data, res, (uint32_t)first, (uint32_t)cap, pf, nd, has_next, J,
+                          j DIAG_PASS);
+        }
         STAMP(5);
+        walk_lanes(data, J, index, res);
+        // the walk's loads are data-dependent in number: drain them here so
+        // that the next batch waits for its header window with a counted
+        // vmcnt, not for every row in flight
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        STAMP(4);
     }
-    ring_producer_done(&ring);
 #ifdef RPGPU_DIAG_STAMPS
     if (lane_id() == 0)
         for (int i = 0; i < 6; i++) atomicAdd(&g_stamps[i], (unsigned long long)sp.st[i]);
@@ -627,7 +610,7 @@ __global__ __launch_bounds__(1024) void block_scan_kernel(uint64_t* __restrict__
 // crc_out[i] = crc32c::Extend(seed[i], data + off[i], len[i])
 // (hashing/crc32c.h:21-43).  Same strided-row scheme; init ~seed folded into
 // the first four bytes, bytes before the range zeroed.
-__global__ __launch_bounds__(kRangesThreads) void crc_ranges_kernel(
+__global__ __launch_bounds__(kValidateThreads) void crc_ranges_kernel(
     const uint8_t* __restrict__ data, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
     const uint32_t* __restrict__ seeds, uint32_t n, uint32_t* __restrict__ out,
     const uint32_t* __restrict__ tables) {
@@ -729,7 +712,7 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
     uint32_t *caps, *local_first;
     uint64_t* block_sum;
     scratch_parts(const_cast<void*>(d_scratch), n, &caps, &local_first, &block_sum);
-    const uint32_t need = (n + kCrcWaves - 1) / kCrcWaves;
+    const uint32_t need = (n + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint32_t g = (uint32_t)grid < need ? (uint32_t)grid : need;
     validate_kernel<<<g, kValidateThreads, 0, s>>>(d_descs, n, d_data, d_res, d_index, local_first, caps,
                                                     block_sum, index_cap, d_tables);
@@ -751,7 +734,7 @@ hipError_t launch_crc_ranges(const uint8_t* d_data, const uint64_t* d_off, const
     if (n == 0) return hipSuccess;
     const uint32_t need = (n + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint32_t g = (uint32_t)grid < need ? (uint32_t)grid : need;
-    crc_ranges_kernel<<<g, kRangesThreads, 0, s>>>(d_data, d_off, d_len, d_seed, n, d_out, d_tables);
+    crc_ranges_kernel<<<g, kValidateThreads, 0, s>>>(d_data, d_off, d_len, d_seed, n, d_out, d_tables);
     return hipGetLastError();
 }
 

@@ -6,18 +6,16 @@
 // bytes/iobuf.cc:136-160 (short copies are silent, lengths truncate to int),
 // as restated by oracle/batch.c walk_records.
 //
-// Work split inside a validate_kernel workgroup: kCrcWaves waves checksum
-// batches (all 64 lanes on one batch) and push every batch that needs a
-// walk into an LDS ring as a WalkJob; one walker wave pops up to 64 jobs at
-// a time and walks them together, lane j over job j.  The walk is a chain
-// of dependent reads (every field's position depends on the previous
-// field's value), so the walker spends most of its time waiting on memory;
-// on its own wave that wait costs the checksum waves nothing, and one batch
-// per lane turns one wave's latency into 64 batches' progress.  Each lane
-// reads its batch through a 32-byte register window reloaded at the cursor
-// when a field would run past it: for records with short keys, one reload
-// per record (at the header count, which the next record's leading fields
-// follow).
+// The validate kernel checksums a group of up to 64 batches one after the
+// other (all 64 lanes on one batch), registering each batch that needs a
+// walk as a WalkJob in lane j of the group.  walk_lanes then walks all of
+// them at once, lane j over batch j.  The walk is a chain of dependent
+// reads (every field's position depends on the previous field's value), so
+// one batch per lane turns one wave's latency into 64 batches' progress.
+// Each lane reads its batch through a 32-byte register window reloaded at
+// the cursor when a field would run past it: for records with short keys,
+// one reload per record (at the header count, which the next record's
+// leading fields follow).
 #ifndef RPGPU_WALK_H
 #define RPGPU_WALK_H
 
@@ -218,104 +216,6 @@ __device__ __forceinline__ void walk_lanes(const uint8_t* __restrict__ data, Wal
         uint32_t* r = reinterpret_cast<uint32_t*>(res + J.b);
         r[0] = (uint32_t)verdict;                                           // .verdict
         r[15] = (J.flags & kJobIndex) ? (cnt < J.cap ? cnt : J.cap) : 0u;  // .index_count
-    }
-}
-
-
-// ---- job ring (LDS, one per workgroup) ----------------------------------
-// Producers (checksum waves) claim a slot with an atomic add on `tail`,
-// wait while the ring is full, write the job and publish it by storing
-// slot + 1 into seq[slot % kRing] (release).  The walker takes the
-// consecutive published slots from `head`, walks them, then advances `head`.
-// `done` counts producers that have finished; the walker exits once every
-// producer is done and every claimed slot is consumed, so every wave of the
-// workgroup reaches the end of the kernel.
-constexpr int kJobWords = 12;
-struct Ring {
-    uint32_t head, tail, done, pad;
-    uint32_t seq[kRing];
-    uint32_t job[kRing][kJobWords];
-};
-
-__device__ __forceinline__ uint32_t lds_load_acq(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_store_rel(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-__device__ __forceinline__ void ring_init(Ring* R) {
-    for (int i = threadIdx.x; i < kRing; i += blockDim.x) R->seq[i] = 0;
-    if (threadIdx.x == 0) R->head = R->tail = R->done = 0;
-}
-
-// Called by a whole checksum wave with a wave-uniform job.
-__device__ __forceinline__ void ring_push(Ring* R, const WalkJob& J) {
-    uint32_t slot = 0;
-    if (lane_id() == 0) slot = __hip_atomic_fetch_add(&R->tail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    slot = __builtin_amdgcn_readfirstlane(slot);
-    // full: the walker frees slots as it finishes jobs
-    while (slot - __builtin_amdgcn_readfirstlane(lds_load_acq(&R->head)) >= (uint32_t)kRing) __builtin_amdgcn_s_sleep(2);
-    if (lane_id() == 0) {
-        uint32_t* w = R->job[slot % kRing];
-        w[0] = (uint32_t)J.body;
-        w[1] = (uint32_t)(J.body >> 32);
-        w[2] = (uint32_t)(uint64_t)J.base_offset;
-        w[3] = (uint32_t)((uint64_t)J.base_offset >> 32);
-        w[4] = (uint32_t)(uint64_t)J.first_ts;
-        w[5] = (uint32_t)((uint64_t)J.first_ts >> 32);
-        w[6] = J.n;
-        w[7] = (uint32_t)J.rc;
-        w[8] = J.first;
-        w[9] = J.cap;
-        w[10] = J.b;
-        w[11] = J.flags;
-        lds_store_rel(&R->seq[slot % kRing], slot + 1);
-    }
-}
-
-__device__ __forceinline__ void ring_producer_done(Ring* R) {
-    if (lane_id() == 0) __hip_atomic_fetch_add(&R->done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// The walker wave's loop.
-__device__ __forceinline__ void walker(Ring* R, const uint8_t* __restrict__ data,
-                                       rpgpu_record_index* __restrict__ index, rpgpu_batch_result* __restrict__ res,
-                                       uint32_t producers) {
-    const uint32_t l = lane_id();
-    uint32_t head = 0;  // only this wave writes R->head
-    for (;;) {
-        const uint32_t slot = head + l;
-        const bool avail = lds_load_acq(&R->seq[slot % kRing]) == slot + 1;
-        // the consecutive published slots from head
-        const uint64_t m = __ballot(avail);
-        const uint32_t take = m == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
-        if (take == 0) {
-            // every producer finished and every claimed slot is consumed
-            const bool all_done = __builtin_amdgcn_readfirstlane(lds_load_acq(&R->done)) == producers;
-            if (all_done && __builtin_amdgcn_readfirstlane(lds_load_acq(&R->tail)) == head) break;
-            __builtin_amdgcn_s_sleep(8);
-            continue;
-        }
-        WalkJob J;
-        J.flags = 0;
-        if (l < take) {
-            const uint32_t* w = R->job[slot % kRing];
-            J.body = (uint64_t)w[1] << 32 | w[0];
-            J.base_offset = (int64_t)((uint64_t)w[3] << 32 | w[2]);
-            J.first_ts = (int64_t)((uint64_t)w[5] << 32 | w[4]);
-            J.n = w[6];
-            J.rc = (int32_t)w[7];
-            J.first = w[8];
-            J.cap = w[9];
-            J.b = w[10];
-            J.flags = w[11];
-        }
-        // the jobs are copied out: free their slots before the (long) walk
-        // so the checksum waves never wait on it
-        head += take;
-        if (l == 0) lds_store_rel(&R->head, head);
-        walk_lanes(data, J, index, res);
     }
 }
 

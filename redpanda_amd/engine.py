@@ -150,8 +150,10 @@ class Engine:
         d_res = torch.zeros(m * 64, dtype=torch.uint8, device=dev)
         d_used = torch.zeros(2, dtype=torch.int64, device=dev)
         d_vscr = torch.zeros(max(self.scratch_bytes(n), 1), dtype=torch.uint8, device=dev)
-        self.validate_device(d_descs.data_ptr(), n, d_data.data_ptr(), d_res.data_ptr(), 0, 0,
-                             d_used.data_ptr(), d_vscr.data_ptr(), sh)
+        index0_cap = int(descs["length"].astype(np.uint64).sum() // 2) + 1
+        d_index0 = torch.zeros(index0_cap * 32, dtype=torch.uint8, device=dev)
+        self.validate_device(d_descs.data_ptr(), n, d_data.data_ptr(), d_res.data_ptr(),
+                             d_index0.data_ptr(), index0_cap, d_used.data_ptr(), d_vscr.data_ptr(), sh)
         d_scr = torch.zeros(max(self.decomp_scratch_bytes(n), 1), dtype=torch.uint8, device=dev)
         self.decomp_plan_device(d_descs.data_ptr(), n, d_data.data_ptr(), d_res.data_ptr(),
                                 d_used.data_ptr(), d_scr.data_ptr(), sh)
