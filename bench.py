@@ -275,7 +275,7 @@ def main() -> int:
                      "traffic": None,
                      "kernel": ("pipeline: validate_kernel + decomp_caps/decomp_kernel + "
                                 "validate_kernel over the rewritten batches" if decompress
-                                else "validate_kernel"),
+                                else "validate_kernel + walk_kernel"),
                      "kernel_ms": round(run_ms, 4),
                      "algorithmic_bytes_per_launch": int(alg_bytes)},
         "cpu_baseline": None,

@@ -22,7 +22,7 @@ namespace rpgpu {
 hipError_t launch_validate(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                            rpgpu_batch_result* d_res, rpgpu_record_index* d_index, uint64_t index_cap,
                            uint64_t* d_index_used, void* d_scratch, const uint32_t* d_tables, int grid,
-                           hipStream_t s);
+                           hipStream_t s, const Overlap* ov);
 hipError_t launch_crc_ranges(const uint8_t* d_data, const uint64_t* d_off, const uint32_t* d_len,
                              const uint32_t* d_seed, uint32_t n, uint32_t* d_out, const uint32_t* d_tables,
                              int grid, hipStream_t s);
@@ -31,7 +31,8 @@ hipError_t launch_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_
                        uint64_t* d_index_used, void* d_scratch, hipStream_t s);
 hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                       rpgpu_batch_result* d_res, rpgpu_record_index* d_index, uint64_t index_cap,
-                      const void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s);
+                      const void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s,
+                      const Overlap* ov);
 size_t decomp_scratch_bytes(uint32_t n);
 hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                               const rpgpu_batch_result* d_vres, uint64_t* d_out_bytes, void* d_scratch,
@@ -40,7 +41,8 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                              const rpgpu_batch_result* d_vres, rpgpu_decomp_result* d_dres, uint8_t* d_out,
                              uint64_t out_cap, rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_vres2,
                              rpgpu_record_index* d_index, uint64_t index_cap, uint64_t* d_index_used,
-                             void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s);
+                             void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s,
+                             const Overlap* ov);
 hipError_t launch_uncompress_bound(uint32_t codec, const uint8_t* d_in, uint64_t n, uint64_t* d_res,
                                    hipStream_t s);
 hipError_t launch_uncompress_one(uint32_t codec, const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint64_t cap,
@@ -88,6 +90,8 @@ struct rpgpu_ctx {
     int cu_count = 0;
     int grid = 0;
     hipStream_t stream = nullptr;
+    rpgpu::Overlap overlap{};  // second stream + events: walks overlap checksums
+    bool have_overlap = false;
     uint32_t* d_tables = nullptr;
     DevBuf work;     // submissions: descs | data | results | index | scratch | used
     DevBuf small;    // scalar mirrors
@@ -139,6 +143,11 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
         delete c;
         return nullptr;
     }
+    c->have_overlap = hipStreamCreateWithFlags(&c->overlap.aux, hipStreamNonBlocking) == hipSuccess;
+    for (int k = 0; c->have_overlap && k <= rpgpu::kRunChunks; k++)
+        c->have_overlap = hipEventCreateWithFlags(&c->overlap.ev[k], hipEventDisableTiming) == hipSuccess;
+    // measured no faster at the default grid: opt-in
+    if (!getenv("RPGPU_OVERLAP")) c->have_overlap = false;
     std::vector<uint32_t> t(rpgpu::kTableWords);
     rpgpu::build_tables(t.data());
     if (hipMalloc(&c->d_tables, sizeof(uint32_t) * t.size()) != hipSuccess ||
@@ -163,6 +172,12 @@ void rpgpu_close(rpgpu_ctx* c) {
     c->small.release();
     c->small_out.release();
     if (c->d_tables) (void)hipFree(c->d_tables);
+    if (c->overlap.aux) {
+        (void)hipStreamSynchronize(c->overlap.aux);
+        (void)hipStreamDestroy(c->overlap.aux);
+    }
+    for (int k = 0; k <= rpgpu::kRunChunks; k++)
+        if (c->overlap.ev[k]) (void)hipEventDestroy(c->overlap.ev[k]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -198,7 +213,8 @@ int32_t rpgpu_validate_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, uin
     if (!c || (n && (!d_descs || !d_data || !d_results || !d_scratch))) return RPGPU_EINVAL;
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     hipError_t e = rpgpu::launch_validate(d_descs, n, d_data, d_results, d_index, d_index ? index_cap : 0,
-                                          d_index_used, d_scratch, c->d_tables, c->grid, s);
+                                          d_index_used, d_scratch, c->d_tables, c->grid, s,
+                                          c->have_overlap ? &c->overlap : nullptr);
     if (e != hipSuccess) return fail(c, e, "validate launch");
     return RPGPU_OK;
 }
@@ -219,7 +235,7 @@ int32_t rpgpu_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, uint32_t
     if (!c || (n && (!d_descs || !d_data || !d_results || !d_scratch))) return RPGPU_EINVAL;
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     hipError_t e = rpgpu::launch_run(d_descs, n, d_data, d_results, d_index, d_index ? index_cap : 0,
-                                     d_scratch, c->d_tables, c->grid, s);
+                                     d_scratch, c->d_tables, c->grid, s, c->have_overlap ? &c->overlap : nullptr);
     if (e != hipSuccess) return fail(c, e, "run launch");
     return RPGPU_OK;
 }
@@ -248,7 +264,8 @@ int32_t rpgpu_decomp_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, u
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     hipError_t e = rpgpu::launch_decomp_run(d_descs, n, d_data, d_results, d_dres, d_out, out_cap, d_out_descs,
                                             d_out_results, d_index, d_index ? index_cap : 0, d_index_used,
-                                            d_scratch, c->d_tables, c->grid, s);
+                                            d_scratch, c->d_tables, c->grid, s,
+                                            c->have_overlap ? &c->overlap : nullptr);
     if (e != hipSuccess) return fail(c, e, "decomp run launch");
     return RPGPU_OK;
 }
@@ -294,7 +311,7 @@ int32_t rpgpu_submit(rpgpu_ctx* c, const rpgpu_batch_desc* descs, uint32_t n, co
                                reinterpret_cast<rpgpu_batch_result*>(base + o_res),
                                reinterpret_cast<rpgpu_record_index*>(base + o_idx), index_cap,
                                reinterpret_cast<uint64_t*>(base + o_used), base + o_scr, c->d_tables,
-                               c->grid, s);
+                               c->grid, s, c->have_overlap ? &c->overlap : nullptr);
     if (e != hipSuccess) return fail(c, e, "validate launch");
     Ticket* t = nullptr;
     for (auto& x : c->tickets)

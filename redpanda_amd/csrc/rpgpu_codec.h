@@ -136,6 +136,41 @@ RPC_HD void copy_match(uint8_t* dst, uint64_t off, uint64_t n) {
     for (uint64_t i = 0; i < n; i += step) st16(dst + i, p);
 }
 
+// ---------------------------------------------------------------- input window
+// The decoders read tokens, lengths and offsets through 32 bytes of input
+// held in registers (one 32-byte load per ~29 bytes of stream instead of a
+// dependent byte load per field); literal and match bytes are copied with
+// wide loads.  Bytes are addressed by input offset; at() reloads the window
+// when a read would run past it.
+struct InWin {
+    uint32_t w0, w1, w2, w3, w4, w5, w6, w7;
+    int64_t pos;
+};
+RPC_HD void win_load(InWin& W, const uint8_t* in, int64_t p) {
+    B16 a, b;
+    ld16(a, in + p);
+    ld16(b, in + p + 16);
+    W.w0 = a.w[0], W.w1 = a.w[1], W.w2 = a.w[2], W.w3 = a.w[3];
+    W.w4 = b.w[0], W.w5 = b.w[1], W.w6 = b.w[2], W.w7 = b.w[3];
+    W.pos = p;
+}
+// dword q (0..8; 8 reads as 0) of the window: selects, not an indexed array
+// (an array would be placed in scratch memory on the device)
+RPC_HD uint32_t win_dword(const InWin& W, uint32_t q) {
+    const uint32_t a = (q & 1) ? W.w1 : W.w0, b = (q & 1) ? W.w3 : W.w2;
+    const uint32_t c = (q & 1) ? W.w5 : W.w4, d = (q & 1) ? W.w7 : W.w6;
+    const uint32_t lo = (q & 2) ? b : a, hi = (q & 2) ? d : c;
+    return q >= 8 ? 0u : ((q & 4) ? hi : lo);
+}
+// 4 input bytes from offset p (little-endian), reloading the window so that
+// [p, p + need) lies inside it (need <= 4)
+RPC_HD uint32_t win_at(InWin& W, const uint8_t* in, int64_t p, int64_t need) {
+    if (p < W.pos || p + need > W.pos + 32) win_load(W, in, p);
+    const uint32_t o = (uint32_t)(p - W.pos), q = o >> 2, sh = 8 * (o & 3);
+    const uint32_t lo = win_dword(W, q);
+    return sh ? (lo >> sh) | (win_dword(W, q + 1) << (32 - sh)) : lo;
+}
+
 // ---------------------------------------------------------------- XXH32
 // xxhash.c XXH32 (one shot; the frame decoder's streaming states hash
 // contiguous data here, which gives the same digest)
@@ -181,7 +216,8 @@ RPC_HD uint32_t xxh32(const uint8_t* p, uint64_t len, uint32_t seed) {
 // ---------------------------------------------------------------- LZ4 block
 // read_variable_length (lz4.c): the safe decoder always checks the loop
 // bound; err = 1 is initial_error, 2 is loop_error.
-RPC_HD uint32_t lz4_varlen(const uint8_t* in, int64_t& ip, int64_t lencheck, bool initial_check, int& err) {
+RPC_HD uint32_t lz4_varlen(InWin& W, const uint8_t* in, int64_t& ip, int64_t lencheck, bool initial_check,
+                           int& err) {
     uint32_t len = 0;  // U32 in lz4.c
     err = 0;
     if (initial_check && ip >= lencheck) {
@@ -190,7 +226,8 @@ RPC_HD uint32_t lz4_varlen(const uint8_t* in, int64_t& ip, int64_t lencheck, boo
     }
     uint32_t s;
     do {
-        s = in[ip++];
+        s = win_at(W, in, ip, 1) & 255u;
+        ip++;
         len += s;
         if (ip >= lencheck) {
             err = 2;
@@ -215,13 +252,16 @@ RPC_HD int64_t lz4_block(const uint8_t* in, int64_t isz, uint8_t* out, int64_t o
     int64_t ip = 0, op = 0, off = 0;
     bool safe = oend < 64;  // FASTLOOP_SAFE_DISTANCE
     int err;
+    InWin W;
+    win_load(W, in, 0);
     for (;;) {
-        const uint32_t token = in[ip++];
+        const uint32_t token = win_at(W, in, ip, 1) & 255u;
+        ip++;
         int64_t len = token >> 4;
         bool lit_checks;  // the literals go through safe_literal_copy
         if (!safe) {
             if (len == 15) {
-                len += lz4_varlen(in, ip, iend - 15, true, err);
+                len += lz4_varlen(W, in, ip, iend - 15, true, err);
                 if (err == 1) return -1;
                 lit_checks = op + len > oend - 32 || ip + len > iend - 32;
             } else {
@@ -235,7 +275,7 @@ RPC_HD int64_t lz4_block(const uint8_t* in, int64_t isz, uint8_t* out, int64_t o
                 op += len;
                 ip += len;
                 len = token & 15;
-                off = le16(in + ip);
+                off = win_at(W, in, ip, 2) & 0xFFFFu;
                 ip += 2;
                 if (len != 15 && off >= 8 && off <= op + hist) {  // match >= lowPrefix
                     copy_match(out + op, (uint64_t)off, (uint64_t)len + 4);
@@ -245,7 +285,7 @@ RPC_HD int64_t lz4_block(const uint8_t* in, int64_t isz, uint8_t* out, int64_t o
                 goto match;
             }
             if (len == 15) {
-                len += lz4_varlen(in, ip, iend - 15, true, err);
+                len += lz4_varlen(W, in, ip, iend - 15, true, err);
                 if (err == 1) return -1;
             }
             lit_checks = true;
@@ -259,12 +299,12 @@ RPC_HD int64_t lz4_block(const uint8_t* in, int64_t isz, uint8_t* out, int64_t o
         copy_fwd(out + op, in + ip, (uint64_t)len);
         ip += len;
         op += len;
-        off = le16(in + ip);
+        off = win_at(W, in, ip, 2) & 0xFFFFu;
         ip += 2;
         len = token & 15;
     match:
         if (len == 15) {
-            len += lz4_varlen(in, ip, iend - 4, false, err);  // iend - LASTLITERALS + 1
+            len += lz4_varlen(W, in, ip, iend - 4, false, err);  // iend - LASTLITERALS + 1
             if (err) return -1;
         }
         len += 4;  // MINMATCH
@@ -483,18 +523,21 @@ RPC_HD bool snappy_varint(const uint8_t* p, uint64_t n, uint32_t& v, uint32_t& u
 // `expected` bytes produced.
 RPC_HD bool snappy_raw(const uint8_t* in, uint64_t n, uint8_t* out, uint32_t expected, uint32_t hdr) {
     uint64_t ip = hdr, op = 0;
+    InWin W;
+    win_load(W, in, (int64_t)ip);
     for (;;) {
         if (ip == n) return op == expected;  // eof at a tag boundary, CheckLength
-        const uint32_t c = in[ip];
+        const uint32_t c = win_at(W, in, (int64_t)ip, 1) & 255u;
         const uint32_t type = c & 3u;
         const uint32_t extra = type == 0 ? ((c >> 2) >= 60 ? (c >> 2) - 59 : 0) : (type == 3 ? 4 : type);
         if (n - ip < extra + 1) return false;
         ip++;
+        // the tag's extra bytes (little-endian, at most 4)
+        const uint32_t x = extra ? win_at(W, in, (int64_t)ip, extra) : 0u;
         if (type == 0) {
             uint32_t len = (c >> 2) + 1;
             if (len >= 61) {
-                uint32_t v = 0;
-                for (uint32_t k = 0; k < extra; k++) v |= (uint32_t)in[ip + k] << (8 * k);
+                const uint32_t v = extra == 4 ? x : x & ((1u << (8 * extra)) - 1);
                 len = v + 1;  // uint32 arithmetic, as ExtractLowBytes(...) + 1
                 ip += extra;
             }
@@ -507,13 +550,13 @@ RPC_HD bool snappy_raw(const uint8_t* in, uint64_t n, uint8_t* out, uint32_t exp
             uint32_t len, off;
             if (type == 1) {
                 len = 4 + ((c >> 2) & 7u);
-                off = ((c >> 5) << 8) | in[ip];
+                off = ((c >> 5) << 8) | (x & 255u);
             } else if (type == 2) {
                 len = (c >> 2) + 1;
-                off = le16(in + ip);
+                off = x & 0xFFFFu;
             } else {
                 len = (c >> 2) + 1;
-                off = le32(in + ip);
+                off = x;
             }
             ip += extra;
             if (off == 0 || op < off) return false;  // Produced() <= offset - 1u

@@ -35,7 +35,8 @@ hipError_t launch_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_
                        uint64_t* d_index_used, void* d_scratch, hipStream_t s);
 hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                       rpgpu_batch_result* d_res, rpgpu_record_index* d_index, uint64_t index_cap,
-                      const void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s);
+                      const void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s,
+                      const Overlap* ov);
 size_t validate_scratch_bytes(uint32_t n);
 
 namespace {
@@ -222,7 +223,8 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                              const rpgpu_batch_result* d_vres, rpgpu_decomp_result* d_dres, uint8_t* d_out,
                              uint64_t out_cap, rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_vres2,
                              rpgpu_record_index* d_index, uint64_t index_cap, uint64_t* d_index_used,
-                             void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s) {
+                             void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s,
+                             const Overlap* ov) {
     if (n == 0) return d_index_used ? hipMemsetAsync(d_index_used, 0, sizeof(uint64_t), s) : hipSuccess;
     const Parts p = parts(d_scratch, n);
     const uint32_t nblk = (n + 255) / 256;
@@ -231,7 +233,7 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if ((e = launch_plan(d_out_descs, n, d_out, d_index_used, p.vscratch, s)) != hipSuccess) return e;
-    if ((e = launch_run(d_out_descs, n, d_out, d_vres2, d_index, index_cap, p.vscratch, d_tables, grid, s)) !=
+    if ((e = launch_run(d_out_descs, n, d_out, d_vres2, d_index, index_cap, p.vscratch, d_tables, grid, s, ov)) !=
         hipSuccess)
         return e;
     decomp_patch_kernel<<<nblk, 256, 0, s>>>(d_dres, d_vres2, n, d_out);

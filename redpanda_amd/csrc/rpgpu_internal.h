@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "rpgpu.h"
+#include <hip/hip_runtime.h>
 
 namespace rpgpu {
 
@@ -34,6 +35,16 @@ constexpr int kWavesPerBlock = kValidateThreads / 64;
 constexpr int kBlocksPerCU = 4;        // default grid: 16 waves per CU
 constexpr int kGroup = 64;             // batches per wave between record walks (one per lane)
 constexpr int kScanBlock = 1024;
+
+// launch_run: the arena is checksummed in kRunChunks launches and each
+// chunk's record walk overlaps the next chunk's checksums on a second stream
+// (arenas of at least kRunChunkMin batches)
+constexpr int kRunChunks = 4;
+constexpr uint32_t kRunChunkMin = 16384;
+struct Overlap {
+    hipStream_t aux;
+    hipEvent_t ev[kRunChunks + 1];
+};
 
 void build_tables(uint32_t* out /* kTableWords */);
 

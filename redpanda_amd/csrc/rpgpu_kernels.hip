@@ -22,7 +22,10 @@
 // batch's) rows are loaded into the registers each row frees as it is
 // checksummed, so 8 KiB per wave stay in flight.
 //
-// (2) Record walk (rpgpu_walk.h), one lane per batch of the group.
+// (2) Record walk (rpgpu_walk.h): walk_kernel, a separate launch with one
+// lane per batch over the whole arena.  The walk is a chain of dependent
+// reads; spread over a lane per batch it is hidden by occupancy instead of
+// stalling the checksum stream of the wave that owns the batch.
 //
 // RPGPU_OP_RECRC (the rewritten batches of rpgpu_decomp_run_device): the
 // header CRC is not checked but computed after the Kafka CRC, over a header
@@ -219,12 +222,13 @@ __device__ __forceinline__ u32x4 merge_header(u32x4 y, int32_t ro0, uint32_t v_i
 
 // Checksums one batch whose header window and first rows are in `pf` and,
 // as the rows free their registers, loads the next batch's rows into them.
-// A batch that needs a record walk becomes lane j's WalkJob.
+// A batch that needs a record walk is left at verdict OK / index_count 0
+// for walk_kernel.
 __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, const rpgpu_batch_desc& d,
                                               uint32_t b, const uint8_t* __restrict__ data,
                                               rpgpu_batch_result* __restrict__ res, uint32_t index_first,
-                                              uint32_t cap, Prefetch& pf, const rpgpu_batch_desc& nd,
-                                              bool has_next, WalkJob& J, uint32_t j DIAG_PARAM) {
+                                              Prefetch& pf, const rpgpu_batch_desc& nd,
+                                              bool has_next DIAG_PARAM) {
     const uint32_t l = lane_id();
     const uint8_t* p = data + d.offset;
     const uint32_t len = d.length;
@@ -436,20 +440,6 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
         r.verdict = RPGPU_V_BODY_TRUNC_THROW;
     } else if (codec > 4) {
         r.verdict = RPGPU_V_BAD_CODEC_THROW;
-    } else if (codec == 0 && (d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX))) {
-        // walked with the rest of the group; the walk patches verdict and
-        // index_count
-        if (l == j) {
-            J.body = d.offset + kHeaderSize;
-            J.base_offset = r.h.base_offset;
-            J.first_ts = r.h.first_ts;
-            J.n = (uint32_t)(n - kHeaderSize);
-            J.rc = r.h.record_count;
-            J.first = index_first;
-            J.cap = cap;
-            J.b = b;
-            J.flags = kJobLive | ((d.ops & RPGPU_OP_INDEX) ? kJobIndex : 0u);
-        }
     }
     write_result(res + b, r);
     STAMP(3);
@@ -459,7 +449,7 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
 // together.  index_first[i] = local exclusive prefix, block_base[i /
 // kScanBlock] = prefix of earlier scan blocks.
 __global__ __launch_bounds__(kValidateThreads) void validate_kernel(
-    const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
+    const rpgpu_batch_desc* __restrict__ descs, uint32_t b0, uint32_t n, const uint8_t* __restrict__ data,
     rpgpu_batch_result* __restrict__ res, rpgpu_record_index* __restrict__ index,
     const uint32_t* __restrict__ local_first, const uint32_t* __restrict__ caps,
     const uint64_t* __restrict__ block_base, uint64_t index_cap, const uint32_t* __restrict__ tables) {
@@ -474,46 +464,70 @@ __global__ __launch_bounds__(kValidateThreads) void validate_kernel(
 #endif
     Prefetch pf;
     pf.gm = Geom{0, 0};
-    if (gw < n) {
-        const rpgpu_batch_desc d0 = sload_desc(descs + gw);
+    if (b0 + gw < n) {
+        const rpgpu_batch_desc d0 = sload_desc(descs + b0 + gw);
         const uint8_t* p0 = data + d0.offset;
         const __amdgpu_buffer_rsrc_t rs0 = batch_rsrc(p0);
         pf.hv = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs0, (int32_t)(4 * (lane_id() & 15)), 0, 0);
         pf.gm = desc_geometry(d0);
         load_rows(pf.x, rs0, pf.gm, 0, lane_id());
     }
-    for (uint32_t g = gw; g < n; g += kGroup * nw) {
-        WalkJob J;
-        J.flags = 0;
-        for (uint32_t j = 0; j < (uint32_t)kGroup; j++) {
-            const uint32_t b = g + j * nw;
-            if (b >= n) break;
-            const rpgpu_batch_desc d = sload_desc(descs + b);
-            const bool has_next = b + nw < n;
-            // always loaded (the batch's own descriptor when there is no
-            // next one; has_next masks its use): a conditionally initialised
-            // struct is lowered to scratch memory
-            const rpgpu_batch_desc nd = sload_desc(descs + (has_next ? b + nw : b));
-            const uint64_t first = sload(block_base + b / kScanBlock) + sload(local_first + b);
-            // never write past the caller's index buffer (rpgpu_validate_device)
-            uint64_t cap = sload(caps + b);
-            if (first >= index_cap) cap = 0;
-            else if (first + cap > index_cap) cap = index_cap - first;
-            process_batch(sT, d, b, data, res, (uint32_t)first, (uint32_t)cap, pf, nd, has_next, J,
-                          j DIAG_PASS);
-        }
+    for (uint32_t b = b0 + gw; b < n; b += nw) {
+        const rpgpu_batch_desc d = sload_desc(descs + b);
+        const bool has_next = b + nw < n;
+        // always loaded (the batch's own descriptor when there is no next
+        // one; has_next masks its use): a conditionally initialised struct
+        // is lowered to scratch memory
+        const rpgpu_batch_desc nd = sload_desc(descs + (has_next ? b + nw : b));
+        const uint64_t first = sload(block_base + b / kScanBlock) + sload(local_first + b);
+        process_batch(sT, d, b, data, res, (uint32_t)first, pf, nd, has_next DIAG_PASS);
         STAMP(5);
-        walk_lanes(data, J, index, res);
-        // the walk's loads are data-dependent in number: drain them here so
-        // that the next batch waits for its header window with a counted
-        // vmcnt, not for every row in flight
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-        STAMP(4);
     }
 #ifdef RPGPU_DIAG_STAMPS
     if (lane_id() == 0)
         for (int i = 0; i < 6; i++) atomicAdd(&g_stamps[i], (unsigned long long)sp.st[i]);
 #endif
+}
+
+// One lane per batch: the record walk of every batch that needs one and
+// passed validation (verdict OK, uncompressed).  Writes the batch's verdict
+// and index_count; the index slice is the plan's (index_cap clamps it to
+// the caller's buffer, as in rpgpu_validate_device).
+__global__ __launch_bounds__(256) void walk_kernel(const rpgpu_batch_desc* __restrict__ descs, uint32_t b0,
+                                                   uint32_t n,
+                                                   const uint8_t* __restrict__ data,
+                                                   rpgpu_batch_result* __restrict__ res,
+                                                   rpgpu_record_index* __restrict__ index,
+                                                   const uint32_t* __restrict__ local_first,
+                                                   const uint32_t* __restrict__ caps,
+                                                   const uint64_t* __restrict__ block_base, uint64_t index_cap) {
+    const uint32_t b = b0 + blockIdx.x * blockDim.x + threadIdx.x;
+    WalkJob J;
+    J.flags = 0;
+    J.body = 0;
+    J.base_offset = J.first_ts = 0;
+    J.n = J.first = J.cap = J.b = 0;
+    J.rc = 0;
+    if (b < n) {
+        const rpgpu_batch_desc d = descs[b];
+        const rpgpu_batch_result& r = res[b];
+        if ((d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX)) && r.verdict == RPGPU_V_OK && r.codec == 0) {
+            const uint64_t first = block_base[b / kScanBlock] + local_first[b];
+            uint64_t cap = caps[b];
+            if (first >= index_cap) cap = 0;
+            else if (first + cap > index_cap) cap = index_cap - first;
+            J.body = d.offset + kHeaderSize;
+            J.base_offset = r.base_offset;
+            J.first_ts = r.first_timestamp;
+            J.n = (uint32_t)r.size_bytes - kHeaderSize;  // verdict OK: the trimmed batch length
+            J.rc = r.record_count;
+            J.first = (uint32_t)first;
+            J.cap = (uint32_t)cap;
+            J.b = b;
+            J.flags = kJobLive | ((d.ops & RPGPU_OP_INDEX) ? kJobIndex : 0u);
+        }
+    }
+    walk_lanes(data, J, index, res);
 }
 
 // ------------------------------------------------------- index-cap prepass
@@ -705,27 +719,51 @@ hipError_t launch_block_scan(uint64_t* block_sum, uint32_t nb, uint64_t* total, 
     return hipGetLastError();
 }
 
+// The walk of a chunk of batches runs on the overlap stream while the next
+// chunk is checksummed: the walk is latency-bound, the checksum
+// bandwidth-bound, and the two share the CUs (validate_kernel leaves room:
+// kBlocksPerCU workgroups of 4 waves at <= 80 VGPRs).
 hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                       rpgpu_batch_result* d_res, rpgpu_record_index* d_index, uint64_t index_cap,
-                      const void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s) {
+                      const void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s,
+                      const Overlap* ov) {
     if (n == 0) return hipSuccess;
     uint32_t *caps, *local_first;
     uint64_t* block_sum;
     scratch_parts(const_cast<void*>(d_scratch), n, &caps, &local_first, &block_sum);
-    const uint32_t need = (n + kWavesPerBlock - 1) / kWavesPerBlock;
-    const uint32_t g = (uint32_t)grid < need ? (uint32_t)grid : need;
-    validate_kernel<<<g, kValidateThreads, 0, s>>>(d_descs, n, d_data, d_res, d_index, local_first, caps,
-                                                    block_sum, index_cap, d_tables);
-    return hipGetLastError();
+    const uint32_t chunks = (ov && n >= kRunChunkMin) ? (uint32_t)kRunChunks : 1u;
+    hipError_t e = hipSuccess;
+    for (uint32_t k = 0; k < chunks; k++) {
+        const uint32_t lo = (uint32_t)((uint64_t)n * k / chunks), hi = (uint32_t)((uint64_t)n * (k + 1) / chunks);
+        const uint32_t need = (hi - lo + kWavesPerBlock - 1) / kWavesPerBlock;
+        const uint32_t g = (uint32_t)grid < need ? (uint32_t)grid : need;
+        validate_kernel<<<g, kValidateThreads, 0, s>>>(d_descs, lo, hi, d_data, d_res, d_index, local_first, caps,
+                                                        block_sum, index_cap, d_tables);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipStream_t ws = s;
+        if (chunks > 1) {
+            if ((e = hipEventRecord(ov->ev[k], s)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(ov->aux, ov->ev[k], 0)) != hipSuccess) return e;
+            ws = ov->aux;
+        }
+        walk_kernel<<<(hi - lo + 255) / 256, 256, 0, ws>>>(d_descs, lo, hi, d_data, d_res, d_index, local_first,
+                                                           caps, block_sum, index_cap);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (chunks > 1) {  // the caller's stream sees the last walk
+        if ((e = hipEventRecord(ov->ev[kRunChunks], ov->aux)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(s, ov->ev[kRunChunks], 0)) != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_validate(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                            rpgpu_batch_result* d_res, rpgpu_record_index* d_index, uint64_t index_cap,
                            uint64_t* d_index_used, void* d_scratch, const uint32_t* d_tables, int grid,
-                           hipStream_t s) {
+                           hipStream_t s, const Overlap* ov) {
     hipError_t e = launch_plan(d_descs, n, d_data, d_index_used, d_scratch, s);
     if (e != hipSuccess) return e;
-    return launch_run(d_descs, n, d_data, d_res, d_index, index_cap, d_scratch, d_tables, grid, s);
+    return launch_run(d_descs, n, d_data, d_res, d_index, index_cap, d_scratch, d_tables, grid, s, ov);
 }
 
 hipError_t launch_crc_ranges(const uint8_t* d_data, const uint64_t* d_off, const uint32_t* d_len,
