@@ -32,7 +32,7 @@ static_assert(kTableWords % 4 == 0, "table blob is copied as 16-byte words");
 
 constexpr int kValidateThreads = 256;  // 4 waves per workgroup
 constexpr int kWavesPerBlock = kValidateThreads / 64;
-constexpr int kBlocksPerCU = 4;        // default grid: 16 waves per CU
+constexpr int kBlocksPerCU = 8;  // default grid: workgroups of 4 waves per CU
 constexpr int kGroup = 64;             // batches per wave between record walks (one per lane)
 constexpr int kScanBlock = 1024;
 
