@@ -34,6 +34,7 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
                       const void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s,
                       const Overlap* ov);
 size_t decomp_scratch_bytes(uint32_t n);
+hipError_t validate_occupancy(int* blocks_per_cu);
 hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                               const rpgpu_batch_result* d_vres, uint64_t* d_out_bytes, void* d_scratch,
                               hipStream_t s);
@@ -138,13 +139,22 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
         const int v = atoi(e);
         if (v >= 1 && v <= 32) bpc = v;
     }
+    // no more workgroups than fit at once (a persistent grid whose tail
+    // waits for a free slot would serialise)
+    int fit = 0;
+    if (rpgpu::validate_occupancy(&fit) == hipSuccess && fit >= 1 && fit < bpc) bpc = fit;
     c->grid = c->cu_count * bpc;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return nullptr;
     }
+    c->overlap.chunks = 4;
+    if (const char* e = getenv("RPGPU_RUN_CHUNKS")) {
+        const int v = atoi(e);
+        if (v >= 1 && v <= rpgpu::kMaxRunChunks) c->overlap.chunks = v;
+    }
     c->have_overlap = hipStreamCreateWithFlags(&c->overlap.aux, hipStreamNonBlocking) == hipSuccess;
-    for (int k = 0; c->have_overlap && k <= rpgpu::kRunChunks; k++)
+    for (int k = 0; c->have_overlap && k <= c->overlap.chunks; k++)
         c->have_overlap = hipEventCreateWithFlags(&c->overlap.ev[k], hipEventDisableTiming) == hipSuccess;
     // measured no faster at the default grid: opt-in
     if (!getenv("RPGPU_OVERLAP")) c->have_overlap = false;
@@ -176,7 +186,7 @@ void rpgpu_close(rpgpu_ctx* c) {
         (void)hipStreamSynchronize(c->overlap.aux);
         (void)hipStreamDestroy(c->overlap.aux);
     }
-    for (int k = 0; k <= rpgpu::kRunChunks; k++)
+    for (int k = 0; k <= rpgpu::kMaxRunChunks; k++)
         if (c->overlap.ev[k]) (void)hipEventDestroy(c->overlap.ev[k]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;

@@ -39,11 +39,12 @@ constexpr int kScanBlock = 1024;
 // launch_run: the arena is checksummed in kRunChunks launches and each
 // chunk's record walk overlaps the next chunk's checksums on a second stream
 // (arenas of at least kRunChunkMin batches)
-constexpr int kRunChunks = 4;
+constexpr int kMaxRunChunks = 256;
 constexpr uint32_t kRunChunkMin = 16384;
 struct Overlap {
     hipStream_t aux;
-    hipEvent_t ev[kRunChunks + 1];
+    int chunks;  // chunks per launch_run (RPGPU_RUN_CHUNKS)
+    hipEvent_t ev[kMaxRunChunks + 1];
 };
 
 void build_tables(uint32_t* out /* kTableWords */);

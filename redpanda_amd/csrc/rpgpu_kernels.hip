@@ -776,6 +776,10 @@ hipError_t launch_crc_ranges(const uint8_t* d_data, const uint64_t* d_off, const
     return hipGetLastError();
 }
 
+hipError_t validate_occupancy(int* blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, validate_kernel, kValidateThreads, 0);
+}
+
 size_t validate_scratch_bytes(uint32_t n) {
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
     return (((size_t)n * 8 + 15) & ~(size_t)15) + nb * 8 + 64;
