@@ -36,7 +36,7 @@ constexpr int kBlocksPerCU = 8;  // default grid: workgroups of 4 waves per CU (
 constexpr int kGroup = 64;             // batches per wave between record walks (one per lane)
 constexpr int kScanBlock = 1024;
 
-// launch_run: the arena is checksummed in kRunChunks launches and each
+// launch_run: the arena is checksummed in Overlap::chunks launches and each
 // chunk's record walk overlaps the next chunk's checksums on a second stream
 // (arenas of at least kRunChunkMin batches)
 constexpr int kMaxRunChunks = 256;

@@ -731,7 +731,7 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
     uint32_t *caps, *local_first;
     uint64_t* block_sum;
     scratch_parts(const_cast<void*>(d_scratch), n, &caps, &local_first, &block_sum);
-    const uint32_t chunks = (ov && n >= kRunChunkMin) ? (uint32_t)kRunChunks : 1u;
+    const uint32_t chunks = (ov && n >= kRunChunkMin) ? (uint32_t)ov->chunks : 1u;
     hipError_t e = hipSuccess;
     for (uint32_t k = 0; k < chunks; k++) {
         const uint32_t lo = (uint32_t)((uint64_t)n * k / chunks), hi = (uint32_t)((uint64_t)n * (k + 1) / chunks);
@@ -751,8 +751,8 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (chunks > 1) {  // the caller's stream sees the last walk
-        if ((e = hipEventRecord(ov->ev[kRunChunks], ov->aux)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(s, ov->ev[kRunChunks], 0)) != hipSuccess) return e;
+        if ((e = hipEventRecord(ov->ev[chunks], ov->aux)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(s, ov->ev[chunks], 0)) != hipSuccess) return e;
     }
     return hipSuccess;
 }
