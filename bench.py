@@ -310,10 +310,11 @@ def main() -> int:
         sdata, sdescs = engine.build_arena(spec, sample_n, first=first, nthreads=nthreads)
         sw = float(sdescs["length"].astype(np.float64).sum())
         caps = np.full(sample_n, 256 << 10, dtype=np.uint64)  # ~64 KiB decompressed per batch
+        obuf = np.zeros(sample_n * ((256 << 10) + 256) + 64, dtype=np.uint8)  # allocated once
 
         def cpu_pass():
             r0, _, _ = orc.validate_arena(sdata, sdescs, nthreads=T, fast_crc=True)
-            return r0, orc.decompress_arena(sdata, sdescs, r0, caps, nthreads=T)
+            return r0, orc.decompress_arena(sdata, sdescs, r0, caps, nthreads=T, out=obuf)
 
         cpu_pass()  # warm-up
         times, passes = [], 0

@@ -151,7 +151,7 @@ def compress(codec: int, data) -> bytes:
 
 
 def decompress_arena(data: np.ndarray, descs: np.ndarray, results: np.ndarray, caps,
-                     codecs=(2, 3), nthreads: int = 1) -> dict:
+                     codecs=(2, 3), nthreads: int = 1, out: np.ndarray | None = None) -> dict:
     """Reference outcome of the decompress path for an arena already validated
     (`results` = validate_arena's or the engine's validation results, which
     agree): storage::internal::maybe_decompress_batch_sync
@@ -169,7 +169,8 @@ def decompress_arena(data: np.ndarray, descs: np.ndarray, results: np.ndarray, c
     offs = np.zeros(n, dtype=np.uint64)
     if n:
         offs[1:] = np.cumsum(slots)[:-1]
-    out = np.zeros(int(slots.sum()) + 64, dtype=np.uint8)
+    if out is None or out.nbytes < int(slots.sum()) + 64:  # reusable output buffer (timing loops)
+        out = np.zeros(int(slots.sum()) + 64, dtype=np.uint8)
     verdicts = np.zeros(n, dtype=np.int32)
     lens = np.zeros(n, dtype=np.uint64)
     rdescs = np.zeros(n, dtype=DESC_DTYPE)
