@@ -89,6 +89,9 @@ enum rpgpu_verdict {
     RPGPU_V_LZ4_TRAILING = 32,     /* unconsumed input after LZ4 frame end        */
     RPGPU_V_DECOMP_UNSUPPORTED = 33,/* codec not implemented on this engine (gzip) */
     RPGPU_V_DECOMP_OVERFLOW = 34,  /* decompressed size exceeds the output slot   */
+    /* multi-batch record sets (kafka/protocol/batch_reader.cc:50-58) */
+    RPGPU_V_SET_HEADER_SHORT = 36, /* < 61 bytes left for the next batch header:
+                                      corrupt_message "Invalid kafka header parsing" */
     RPGPU_V_SKIPPED = 40,          /* not decompressed: no RPGPU_OP_DECOMP, not
                                       validated OK, or not compressed        */
 };
@@ -303,6 +306,37 @@ int32_t rpgpu_decomp_run_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_descs,
  * RPGPU_V_DECOMP_OVERFLOW; `out` then holds the first `cap` bytes). */
 int32_t rpgpu_uncompress(rpgpu_ctx* ctx, int32_t codec, const void* in, size_t n, void* out,
                          size_t cap, size_t* out_len);
+
+/* ---- multi-batch record sets ---------------------------------------------
+ * Replaces kafka::batch_reader (kafka/protocol/batch_reader.cc:50-161) over
+ * the record data of many produce partitions at once.  d_sets[i] (a
+ * rpgpu_batch_desc: offset, length, partition, ops; format must be
+ * RPGPU_FMT_KAFKA_WIRE) is one record set: Kafka v2 batches back to back.
+ * Each is split as read_record_batch_info / consume_batch do (size =
+ * batch_length + 12, shares clamped to the bytes left), every batch is
+ * validated (rpgpu_run_device semantics) and the set's outcome is the first
+ * batch that is not accepted, in order (do_load_slice: corrupt_message), or
+ * RPGPU_V_SET_HEADER_SHORT when < 61 bytes remain after accepted batches. */
+typedef struct rpgpu_record_set_result {
+    int32_t verdict;       /* OK, the failing batch's verdict, or SET_HEADER_SHORT */
+    uint32_t batch_count;  /* batches the set's header chain yields             */
+    uint32_t first_batch;  /* its first batch in the batch arrays               */
+    uint32_t failed_batch; /* index within the set of the first failing batch
+                              (= batch_count when none failed)                  */
+} rpgpu_record_set_result; /* 16 bytes */
+
+size_t rpgpu_record_sets_scratch_bytes(uint32_t nsets);
+/* Plan: *d_nbatches = total batches of all sets (size the batch arrays and
+ * a second scratch of rpgpu_validate_scratch_bytes(*d_nbatches) from it). */
+int32_t rpgpu_record_sets_plan_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_sets, uint32_t nsets,
+                                      const uint8_t* d_data, uint64_t* d_nbatches, void* d_scratch,
+                                      void* hip_stream);
+int32_t rpgpu_record_sets_run_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_sets, uint32_t nsets,
+                                     const uint8_t* d_data, rpgpu_record_set_result* d_set_results,
+                                     rpgpu_batch_desc* d_batch_descs, uint32_t nbatches,
+                                     rpgpu_batch_result* d_batch_results, rpgpu_record_index* d_index,
+                                     uint64_t index_cap, uint64_t* d_index_used, void* d_scratch,
+                                     void* d_batch_scratch, void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -20,6 +20,8 @@ RESULT_DTYPE = np.dtype([("verdict", "<i4"), ("crc", "<u4"), ("crc_expected", "<
                          ("max_timestamp", "<i8"), ("index_first", "<u4"), ("index_count", "<u4")])
 INDEX_DTYPE = np.dtype([("offset", "<i8"), ("timestamp", "<i8"), ("key_off", "<u4"),
                         ("key_len", "<i4"), ("val_off", "<u4"), ("val_len", "<i4")])
+SET_RESULT_DTYPE = np.dtype([("verdict", "<i4"), ("batch_count", "<u4"), ("first_batch", "<u4"),
+                             ("failed_batch", "<u4")])
 RP_HEADER_DTYPE = np.dtype([("header_crc", "<u4"), ("size_bytes", "<i4"), ("base_offset", "<i8"),
                             ("type", "i1"), ("crc", "<i4"), ("attrs", "<i2"),
                             ("last_offset_delta", "<i4"), ("first_timestamp", "<i8"),
@@ -31,7 +33,8 @@ _L = None
 
 
 def build(force: bool = False) -> Path:
-    srcs = [HERE / f for f in ("crc32c.c", "batch.c", "codec.c", "decomp.c", "rporacle.h", "Makefile")]
+    srcs = [HERE / f for f in ("crc32c.c", "batch.c", "codec.c", "decomp.c", "sets.c", "rporacle.h",
+                               "Makefile")]
     if force or not LIB_PATH.exists() or any(s.stat().st_mtime > LIB_PATH.stat().st_mtime for s in srcs):
         r = subprocess.run(["make", "-C", str(HERE), "-s"], capture_output=True, text=True)
         if r.returncode != 0:
@@ -71,6 +74,10 @@ def lib() -> C.CDLL:
         L.orc_compress_bound.restype = sz
         L.orc_compress_bound.argtypes = [C.c_int, sz]
         L.orc_decompress_batches.restype = None
+        L.orc_record_sets_split.restype = u64
+        L.orc_record_sets_split.argtypes = [vp, u32, vp, vp, u64, vp, vp, vp]
+        L.orc_record_sets_reduce.restype = None
+        L.orc_record_sets_reduce.argtypes = [u32, vp, vp, vp, vp, vp]
         L.orc_decompress_batches.argtypes = [vp, u32, vp, vp, u32, vp, vp, vp, vp, vp, vp, C.c_int]
         _L = L
     return _L
@@ -181,3 +188,27 @@ def decompress_arena(data: np.ndarray, descs: np.ndarray, results: np.ndarray, c
     rres, ridx, rused = validate_arena(out, rdescs, nthreads=nthreads)
     return dict(verdicts=verdicts, out_len=lens, out=out, out_descs=rdescs, out_results=rres,
                 index=ridx, used=rused)
+
+
+def record_sets(data: np.ndarray, sets: np.ndarray, nthreads: int = 1) -> dict:
+    """Reference outcome of kafka::batch_reader (kafka/protocol/batch_reader.cc:50-161)
+    for every record set: its batches (descriptors, validation results, index)
+    and the set's outcome (first failing batch, or a short header)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    sets = np.ascontiguousarray(sets, dtype=DESC_DTYPE)
+    n = len(sets)
+    first = np.zeros(n, np.uint32)
+    count = np.zeros(n, np.uint32)
+    short = np.zeros(n, np.uint8)
+    L = lib()
+    total = int(L.orc_record_sets_split(sets.ctypes.data, n, data.ctypes.data, None, 0,
+                                        first.ctypes.data, count.ctypes.data, short.ctypes.data))
+    bdescs = np.zeros(max(total, 1), dtype=DESC_DTYPE)
+    L.orc_record_sets_split(sets.ctypes.data, n, data.ctypes.data, bdescs.ctypes.data, total,
+                            first.ctypes.data, count.ctypes.data, short.ctypes.data)
+    bdescs = bdescs[:total]
+    bres, bidx, bused = validate_arena(data, bdescs, nthreads=nthreads)
+    out = np.zeros(n, dtype=SET_RESULT_DTYPE)
+    L.orc_record_sets_reduce(n, first.ctypes.data, count.ctypes.data, short.ctypes.data,
+                             bres.ctypes.data, out.ctypes.data)
+    return dict(sets=out, batch_descs=bdescs, batch_results=bres, index=bidx, used=bused)

@@ -91,6 +91,16 @@ void orc_decompress_batches(const rpgpu_batch_desc* descs, uint32_t n, const uin
                             const uint64_t* out_off, const uint64_t* out_cap, int32_t* verdicts,
                             uint64_t* out_len, rpgpu_batch_desc* rdescs, int nthreads);
 
+/* kafka::batch_reader (kafka/protocol/batch_reader.cc:50-161): split record
+ * sets into batch descriptors (first/count/short_hdr per set; returns the
+ * total), then the outcome per set from the batches' validation results. */
+uint64_t orc_record_sets_split(const rpgpu_batch_desc* sets, uint32_t n, const uint8_t* data,
+                               rpgpu_batch_desc* out, uint64_t cap, uint32_t* first,
+                               uint32_t* count, uint8_t* short_hdr);
+void orc_record_sets_reduce(uint32_t n, const uint32_t* first, const uint32_t* count,
+                            const uint8_t* short_hdr, const rpgpu_batch_result* bres,
+                            rpgpu_record_set_result* out);
+
 #ifdef __cplusplus
 }
 #endif

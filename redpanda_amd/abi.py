@@ -45,6 +45,7 @@ V_DECOMP_BAD_ALLOC = 31
 V_LZ4_TRAILING = 32
 V_DECOMP_UNSUPPORTED = 33
 V_DECOMP_OVERFLOW = 34
+V_SET_HEADER_SHORT = 36
 V_SKIPPED = 40
 
 VERDICT_NAMES = {v: k for k, v in globals().items() if k.startswith("V_") and isinstance(v, int)}
@@ -73,7 +74,10 @@ RP_HEADER_DTYPE = np.dtype([("header_crc", "<u4"), ("size_bytes", "<i4"), ("base
                             ("record_count", "<i4")])
 DECOMP_RESULT_DTYPE = np.dtype([("verdict", "<i4"), ("codec", "<u4"), ("out_offset", "<u8"),
                                 ("out_len", "<u8"), ("out_cap", "<u8")])
+SET_RESULT_DTYPE = np.dtype([("verdict", "<i4"), ("batch_count", "<u4"), ("first_batch", "<u4"),
+                             ("failed_batch", "<u4")])
 assert DESC_DTYPE.itemsize == 24 and RESULT_DTYPE.itemsize == 64 and DECOMP_RESULT_DTYPE.itemsize == 32
+assert SET_RESULT_DTYPE.itemsize == 16
 assert INDEX_DTYPE.itemsize == 32 and RP_HEADER_DTYPE.itemsize == 61
 
 # ---- batch builder spec (redpanda_amd/csrc/rpgen.h) -------------------------
@@ -160,6 +164,10 @@ def lib() -> C.CDLL:
              _u64, _vp, _vp, _vp)
         _sig(L.rpgpu_uncompress, _i32, _vp, _i32, _vp, C.c_size_t, _vp, C.c_size_t,
              C.POINTER(C.c_size_t))
+        _sig(L.rpgpu_record_sets_scratch_bytes, C.c_size_t, _u32)
+        _sig(L.rpgpu_record_sets_plan_device, _i32, _vp, _vp, _u32, _vp, _vp, _vp, _vp)
+        _sig(L.rpgpu_record_sets_run_device, _i32, _vp, _vp, _u32, _vp, _vp, _vp, _u32, _vp, _vp, _u64,
+             _vp, _vp, _vp, _vp)
         _LIB = L
     return _LIB
 
@@ -186,5 +194,6 @@ EXPORTED = [
     "rpgpu_run_device", "rpgpu_crc32c_ranges_device",
     "rpgpu_crc32c_extend", "rpgpu_internal_header_only_crc", "rpgpu_crc_record_batch",
     "rpgpu_decomp_scratch_bytes", "rpgpu_decomp_plan_device", "rpgpu_decomp_run_device",
-    "rpgpu_uncompress",
+    "rpgpu_uncompress", "rpgpu_record_sets_scratch_bytes", "rpgpu_record_sets_plan_device",
+    "rpgpu_record_sets_run_device",
 ]

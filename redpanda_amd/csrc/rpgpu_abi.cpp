@@ -35,6 +35,14 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
                       const Overlap* ov);
 size_t decomp_scratch_bytes(uint32_t n);
 hipError_t validate_occupancy(int* blocks_per_cu);
+size_t sets_scratch_bytes(uint32_t n);
+hipError_t launch_sets_plan(const rpgpu_batch_desc* d_sets, uint32_t n, const uint8_t* d_data,
+                            uint64_t* d_nbatches, void* d_scratch, hipStream_t s);
+hipError_t launch_sets_run(const rpgpu_batch_desc* d_sets, uint32_t n, const uint8_t* d_data,
+                           rpgpu_record_set_result* d_set_res, rpgpu_batch_desc* d_bdescs, uint32_t nbatches,
+                           rpgpu_batch_result* d_bres, rpgpu_record_index* d_index, uint64_t index_cap,
+                           uint64_t* d_index_used, void* d_scratch, void* d_vscratch, const uint32_t* d_tables,
+                           int grid, hipStream_t s, const Overlap* ov);
 hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                               const rpgpu_batch_result* d_vres, uint64_t* d_out_bytes, void* d_scratch,
                               hipStream_t s);
@@ -277,6 +285,36 @@ int32_t rpgpu_decomp_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, u
                                             d_scratch, c->d_tables, c->grid, s,
                                             c->have_overlap ? &c->overlap : nullptr);
     if (e != hipSuccess) return fail(c, e, "decomp run launch");
+    return RPGPU_OK;
+}
+
+size_t rpgpu_record_sets_scratch_bytes(uint32_t n) { return rpgpu::sets_scratch_bytes(n); }
+
+int32_t rpgpu_record_sets_plan_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_sets, uint32_t n,
+                                      const uint8_t* d_data, uint64_t* d_nbatches, void* d_scratch,
+                                      void* hip_stream) {
+    if (!c || (n && (!d_sets || !d_data || !d_scratch))) return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_sets_plan(d_sets, n, d_data, d_nbatches, d_scratch, s);
+    if (e != hipSuccess) return fail(c, e, "record sets plan launch");
+    return RPGPU_OK;
+}
+
+int32_t rpgpu_record_sets_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_sets, uint32_t n,
+                                     const uint8_t* d_data, rpgpu_record_set_result* d_set_results,
+                                     rpgpu_batch_desc* d_batch_descs, uint32_t nbatches,
+                                     rpgpu_batch_result* d_batch_results, rpgpu_record_index* d_index,
+                                     uint64_t index_cap, uint64_t* d_index_used, void* d_scratch,
+                                     void* d_batch_scratch, void* hip_stream) {
+    if (!c || (n && (!d_sets || !d_data || !d_set_results || !d_scratch)) ||
+        (nbatches && (!d_batch_descs || !d_batch_results || !d_batch_scratch)))
+        return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_sets_run(d_sets, n, d_data, d_set_results, d_batch_descs, nbatches,
+                                          d_batch_results, d_index, d_index ? index_cap : 0, d_index_used,
+                                          d_scratch, d_batch_scratch, c->d_tables, c->grid, s,
+                                          c->have_overlap ? &c->overlap : nullptr);
+    if (e != hipSuccess) return fail(c, e, "record sets run launch");
     return RPGPU_OK;
 }
 

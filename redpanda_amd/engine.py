@@ -182,6 +182,50 @@ class Engine:
             index=d_index.cpu().numpy().view(abi.INDEX_DTYPE)[: min(used, index_cap)].copy(),
             used=used, out_bytes=out_bytes)
 
+    # -- multi-batch record sets (rpgpu_record_sets_plan_device / _run_device) ---------
+    def record_sets(self, data: np.ndarray, sets: np.ndarray) -> dict:
+        """kafka::batch_reader over many record sets on the GPU (device entry
+        points, HBM from torch).  Returns host copies: sets (per-set outcome),
+        batch_descs, batch_results, index, used."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        sets = np.ascontiguousarray(sets, dtype=abi.DESC_DTYPE)
+        n = len(sets)
+        sh = torch.cuda.current_stream(dev).cuda_stream
+        L = self._lib
+        d_data = torch.from_numpy(data.copy()).to(dev)
+        d_sets = torch.from_numpy(sets.view(np.uint8).copy()).to(dev)
+        d_scr = torch.zeros(max(int(L.rpgpu_record_sets_scratch_bytes(n)), 1), dtype=torch.uint8, device=dev)
+        d_cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+        rc = L.rpgpu_record_sets_plan_device(self._ctx, d_sets.data_ptr(), n, d_data.data_ptr(),
+                                             d_cnt.data_ptr(), d_scr.data_ptr(), sh)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_record_sets_plan_device: {rc} {self.last_error()}")
+        torch.cuda.synchronize(dev)
+        nb = int(d_cnt[0].item())
+        m = max(nb, 1)
+        d_bdescs = torch.zeros(m * 24, dtype=torch.uint8, device=dev)
+        d_bres = torch.zeros(m * 64, dtype=torch.uint8, device=dev)
+        d_vscr = torch.zeros(max(self.scratch_bytes(nb), 1), dtype=torch.uint8, device=dev)
+        d_sres = torch.zeros(max(n, 1) * 16, dtype=torch.uint8, device=dev)
+        index_cap = int(sets["length"].astype(np.uint64).sum() // 2) + 1
+        d_index = torch.zeros(index_cap * 32, dtype=torch.uint8, device=dev)
+        rc = L.rpgpu_record_sets_run_device(self._ctx, d_sets.data_ptr(), n, d_data.data_ptr(),
+                                            d_sres.data_ptr(), d_bdescs.data_ptr(), nb, d_bres.data_ptr(),
+                                            d_index.data_ptr(), index_cap, d_cnt.data_ptr() + 8,
+                                            d_scr.data_ptr(), d_vscr.data_ptr(), sh)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_record_sets_run_device: {rc} {self.last_error()}")
+        torch.cuda.synchronize(dev)
+        used = int(d_cnt[1].item())
+        return dict(sets=d_sres.cpu().numpy().view(abi.SET_RESULT_DTYPE)[:n].copy(),
+                    batch_descs=d_bdescs.cpu().numpy().view(abi.DESC_DTYPE)[:nb].copy(),
+                    batch_results=d_bres.cpu().numpy().view(abi.RESULT_DTYPE)[:nb].copy(),
+                    index=d_index.cpu().numpy().view(abi.INDEX_DTYPE)[: min(used, index_cap)].copy(),
+                    used=used)
+
     # -- synchronous scalar mirrors ---------------------------------------------------
     def uncompress(self, codec: int, data: bytes | np.ndarray, cap: int | None = None) -> tuple[int, bytes]:
         """compression::compressor::uncompress on the GPU: (verdict, bytes)."""
