@@ -92,6 +92,8 @@ enum rpgpu_verdict {
     /* multi-batch record sets (kafka/protocol/batch_reader.cc:50-58) */
     RPGPU_V_SET_HEADER_SHORT = 36, /* < 61 bytes left for the next batch header:
                                       corrupt_message "Invalid kafka header parsing" */
+    /* segment index (storage/index_state.cc:48-54) */
+    RPGPU_V_INDEX_OFFSET_BELOW_BASE = 37, /* vassert: batch base offset below the segment's */
     RPGPU_V_SKIPPED = 40,          /* not decompressed: no RPGPU_OP_DECOMP, not
                                       validated OK, or not compressed        */
 };
@@ -337,6 +339,46 @@ int32_t rpgpu_record_sets_run_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_s
                                      rpgpu_batch_result* d_batch_results, rpgpu_record_index* d_index,
                                      uint64_t index_cap, uint64_t* d_index_used, void* d_scratch,
                                      void* d_batch_scratch, void* hip_stream);
+
+/* ---- segment offset/time index --------------------------------------------
+ * Replaces segment_index::maybe_track (storage/segment_index.cc:98-120) +
+ * index_state::maybe_index (storage/index_state.cc:38-109) over recovered
+ * on-disk batches, as log_replayer feeds them (storage/log_replayer.cc:26-92).
+ * Segment s covers descriptors [first_batch, first_batch + batch_count) of
+ * a validated arena (d_results of rpgpu_run_device); its batches are tracked
+ * in order up to the first one whose verdict is not OK.  Entries of segment
+ * s are written from d_entries + first_batch (at most one per batch). */
+typedef struct rpgpu_segment {
+    uint32_t first_batch, batch_count;
+    int64_t base_offset;    /* index_state base_offset (the segment's)       */
+    uint64_t file_base;     /* arena offset of file position 0               */
+    uint32_t step;          /* segment_index step (default 4096 * 8)         */
+    uint8_t internal_topic; /* path().is_internal_topic()                     */
+    uint8_t with_offset;    /* offset_delta_time (index_state.h:28-70)       */
+    uint16_t reserved;
+} rpgpu_segment;            /* 32 bytes */
+
+typedef struct rpgpu_segment_state {
+    int32_t status;         /* OK or RPGPU_V_INDEX_OFFSET_BELOW_BASE          */
+    uint32_t entries;       /* index entries written                          */
+    uint32_t tracked;       /* batches tracked                                */
+    uint8_t monotonic;      /* batch_timestamps_are_monotonic                 */
+    uint8_t non_data_timestamps;
+    uint16_t reserved;
+    int64_t max_offset, base_timestamp, max_timestamp;
+    uint64_t acc;           /* segment_index _acc after the last batch       */
+} rpgpu_segment_state;      /* 48 bytes */
+
+typedef struct rpgpu_index_entry {
+    uint32_t relative_offset; /* batch base offset - segment base offset     */
+    uint32_t relative_time;   /* offset_time_index raw value                  */
+    uint64_t position;        /* file position of the batch                   */
+} rpgpu_index_entry;          /* 16 bytes */
+
+int32_t rpgpu_segment_index_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_descs,
+                                   const rpgpu_batch_result* d_results, const rpgpu_segment* d_segs,
+                                   uint32_t nsegs, rpgpu_segment_state* d_states,
+                                   rpgpu_index_entry* d_entries, void* hip_stream);
 
 #ifdef __cplusplus
 }

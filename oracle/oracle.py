@@ -22,6 +22,14 @@ INDEX_DTYPE = np.dtype([("offset", "<i8"), ("timestamp", "<i8"), ("key_off", "<u
                         ("key_len", "<i4"), ("val_off", "<u4"), ("val_len", "<i4")])
 SET_RESULT_DTYPE = np.dtype([("verdict", "<i4"), ("batch_count", "<u4"), ("first_batch", "<u4"),
                              ("failed_batch", "<u4")])
+SEGMENT_DTYPE = np.dtype([("first_batch", "<u4"), ("batch_count", "<u4"), ("base_offset", "<i8"),
+                          ("file_base", "<u8"), ("step", "<u4"), ("internal_topic", "u1"),
+                          ("with_offset", "u1"), ("reserved", "<u2")])
+SEGMENT_STATE_DTYPE = np.dtype([("status", "<i4"), ("entries", "<u4"), ("tracked", "<u4"),
+                                ("monotonic", "u1"), ("non_data_timestamps", "u1"), ("reserved", "<u2"),
+                                ("max_offset", "<i8"), ("base_timestamp", "<i8"), ("max_timestamp", "<i8"),
+                                ("acc", "<u8")])
+INDEX_ENTRY_DTYPE = np.dtype([("relative_offset", "<u4"), ("relative_time", "<u4"), ("position", "<u8")])
 RP_HEADER_DTYPE = np.dtype([("header_crc", "<u4"), ("size_bytes", "<i4"), ("base_offset", "<i8"),
                             ("type", "i1"), ("crc", "<i4"), ("attrs", "<i2"),
                             ("last_offset_delta", "<i4"), ("first_timestamp", "<i8"),
@@ -33,7 +41,7 @@ _L = None
 
 
 def build(force: bool = False) -> Path:
-    srcs = [HERE / f for f in ("crc32c.c", "batch.c", "codec.c", "decomp.c", "sets.c", "rporacle.h",
+    srcs = [HERE / f for f in ("crc32c.c", "batch.c", "codec.c", "decomp.c", "sets.c", "index.c", "rporacle.h",
                                "Makefile")]
     if force or not LIB_PATH.exists() or any(s.stat().st_mtime > LIB_PATH.stat().st_mtime for s in srcs):
         r = subprocess.run(["make", "-C", str(HERE), "-s"], capture_output=True, text=True)
@@ -77,6 +85,8 @@ def lib() -> C.CDLL:
         L.orc_record_sets_split.restype = u64
         L.orc_record_sets_split.argtypes = [vp, u32, vp, vp, u64, vp, vp, vp]
         L.orc_record_sets_reduce.restype = None
+        L.orc_segment_index.restype = None
+        L.orc_segment_index.argtypes = [vp, vp, vp, u32, vp, vp]
         L.orc_record_sets_reduce.argtypes = [u32, vp, vp, vp, vp, vp]
         L.orc_decompress_batches.argtypes = [vp, u32, vp, vp, u32, vp, vp, vp, vp, vp, vp, C.c_int]
         _L = L
@@ -212,3 +222,16 @@ def record_sets(data: np.ndarray, sets: np.ndarray, nthreads: int = 1) -> dict:
     L.orc_record_sets_reduce(n, first.ctypes.data, count.ctypes.data, short.ctypes.data,
                              bres.ctypes.data, out.ctypes.data)
     return dict(sets=out, batch_descs=bdescs, batch_results=bres, index=bidx, used=bused)
+
+
+def segment_index(descs: np.ndarray, results: np.ndarray, segs: np.ndarray):
+    """segment_index::maybe_track over each segment's recovered batches:
+    (states, entries) with entries laid out one slot per batch."""
+    descs = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+    results = np.ascontiguousarray(results, dtype=RESULT_DTYPE)
+    segs = np.ascontiguousarray(segs, dtype=SEGMENT_DTYPE)
+    states = np.zeros(len(segs), dtype=SEGMENT_STATE_DTYPE)
+    entries = np.zeros(max(len(descs), 1), dtype=INDEX_ENTRY_DTYPE)
+    lib().orc_segment_index(descs.ctypes.data, results.ctypes.data, segs.ctypes.data, len(segs),
+                            states.ctypes.data, entries.ctypes.data)
+    return states, entries[:len(descs)]

@@ -101,6 +101,12 @@ void orc_record_sets_reduce(uint32_t n, const uint32_t* first, const uint32_t* c
                             const uint8_t* short_hdr, const rpgpu_batch_result* bres,
                             rpgpu_record_set_result* out);
 
+/* segment_index::maybe_track / index_state::maybe_index per segment
+ * (storage/segment_index.cc:98-120, storage/index_state.cc:38-109) */
+void orc_segment_index(const rpgpu_batch_desc* descs, const rpgpu_batch_result* res,
+                       const rpgpu_segment* segs, uint32_t nsegs, rpgpu_segment_state* states,
+                       rpgpu_index_entry* entries);
+
 #ifdef __cplusplus
 }
 #endif

@@ -46,6 +46,7 @@ V_LZ4_TRAILING = 32
 V_DECOMP_UNSUPPORTED = 33
 V_DECOMP_OVERFLOW = 34
 V_SET_HEADER_SHORT = 36
+V_INDEX_OFFSET_BELOW_BASE = 37
 V_SKIPPED = 40
 
 VERDICT_NAMES = {v: k for k, v in globals().items() if k.startswith("V_") and isinstance(v, int)}
@@ -78,6 +79,15 @@ SET_RESULT_DTYPE = np.dtype([("verdict", "<i4"), ("batch_count", "<u4"), ("first
                              ("failed_batch", "<u4")])
 assert DESC_DTYPE.itemsize == 24 and RESULT_DTYPE.itemsize == 64 and DECOMP_RESULT_DTYPE.itemsize == 32
 assert SET_RESULT_DTYPE.itemsize == 16
+SEGMENT_DTYPE = np.dtype([("first_batch", "<u4"), ("batch_count", "<u4"), ("base_offset", "<i8"),
+                          ("file_base", "<u8"), ("step", "<u4"), ("internal_topic", "u1"),
+                          ("with_offset", "u1"), ("reserved", "<u2")])
+SEGMENT_STATE_DTYPE = np.dtype([("status", "<i4"), ("entries", "<u4"), ("tracked", "<u4"),
+                                ("monotonic", "u1"), ("non_data_timestamps", "u1"), ("reserved", "<u2"),
+                                ("max_offset", "<i8"), ("base_timestamp", "<i8"), ("max_timestamp", "<i8"),
+                                ("acc", "<u8")])
+INDEX_ENTRY_DTYPE = np.dtype([("relative_offset", "<u4"), ("relative_time", "<u4"), ("position", "<u8")])
+assert SEGMENT_DTYPE.itemsize == 32 and SEGMENT_STATE_DTYPE.itemsize == 48 and INDEX_ENTRY_DTYPE.itemsize == 16
 assert INDEX_DTYPE.itemsize == 32 and RP_HEADER_DTYPE.itemsize == 61
 
 # ---- batch builder spec (redpanda_amd/csrc/rpgen.h) -------------------------
@@ -164,6 +174,7 @@ def lib() -> C.CDLL:
              _u64, _vp, _vp, _vp)
         _sig(L.rpgpu_uncompress, _i32, _vp, _i32, _vp, C.c_size_t, _vp, C.c_size_t,
              C.POINTER(C.c_size_t))
+        _sig(L.rpgpu_segment_index_device, _i32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp)
         _sig(L.rpgpu_record_sets_scratch_bytes, C.c_size_t, _u32)
         _sig(L.rpgpu_record_sets_plan_device, _i32, _vp, _vp, _u32, _vp, _vp, _vp, _vp)
         _sig(L.rpgpu_record_sets_run_device, _i32, _vp, _vp, _u32, _vp, _vp, _vp, _u32, _vp, _vp, _u64,
@@ -195,5 +206,5 @@ EXPORTED = [
     "rpgpu_crc32c_extend", "rpgpu_internal_header_only_crc", "rpgpu_crc_record_batch",
     "rpgpu_decomp_scratch_bytes", "rpgpu_decomp_plan_device", "rpgpu_decomp_run_device",
     "rpgpu_uncompress", "rpgpu_record_sets_scratch_bytes", "rpgpu_record_sets_plan_device",
-    "rpgpu_record_sets_run_device",
+    "rpgpu_record_sets_run_device", "rpgpu_segment_index_device",
 ]

@@ -35,6 +35,9 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
                       const Overlap* ov);
 size_t decomp_scratch_bytes(uint32_t n);
 hipError_t validate_occupancy(int* blocks_per_cu);
+hipError_t launch_segment_index(const rpgpu_batch_desc* d_descs, const rpgpu_batch_result* d_res,
+                                const rpgpu_segment* d_segs, uint32_t nsegs, rpgpu_segment_state* d_states,
+                                rpgpu_index_entry* d_entries, hipStream_t s);
 size_t sets_scratch_bytes(uint32_t n);
 hipError_t launch_sets_plan(const rpgpu_batch_desc* d_sets, uint32_t n, const uint8_t* d_data,
                             uint64_t* d_nbatches, void* d_scratch, hipStream_t s);
@@ -315,6 +318,17 @@ int32_t rpgpu_record_sets_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_set
                                           d_scratch, d_batch_scratch, c->d_tables, c->grid, s,
                                           c->have_overlap ? &c->overlap : nullptr);
     if (e != hipSuccess) return fail(c, e, "record sets run launch");
+    return RPGPU_OK;
+}
+
+int32_t rpgpu_segment_index_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs,
+                                   const rpgpu_batch_result* d_results, const rpgpu_segment* d_segs,
+                                   uint32_t nsegs, rpgpu_segment_state* d_states,
+                                   rpgpu_index_entry* d_entries, void* hip_stream) {
+    if (!c || (nsegs && (!d_descs || !d_results || !d_segs || !d_states || !d_entries))) return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_segment_index(d_descs, d_results, d_segs, nsegs, d_states, d_entries, s);
+    if (e != hipSuccess) return fail(c, e, "segment index launch");
     return RPGPU_OK;
 }
 

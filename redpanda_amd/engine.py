@@ -226,6 +226,38 @@ class Engine:
                     index=d_index.cpu().numpy().view(abi.INDEX_DTYPE)[: min(used, index_cap)].copy(),
                     used=used)
 
+    # -- segment offset/time index (rpgpu_segment_index_device) -----------------------
+    def segment_index(self, data: np.ndarray, descs: np.ndarray, segs: np.ndarray) -> dict:
+        """Validate on-disk batches, then build each segment's offset/time index on
+        the GPU.  Returns host copies: results, states, entries (one slot per batch)."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        descs = np.ascontiguousarray(descs, dtype=abi.DESC_DTYPE)
+        segs = np.ascontiguousarray(segs, dtype=abi.SEGMENT_DTYPE)
+        n, ns = len(descs), len(segs)
+        sh = torch.cuda.current_stream(dev).cuda_stream
+        d_data = torch.from_numpy(data.copy()).to(dev)
+        d_descs = torch.from_numpy(descs.view(np.uint8).copy()).to(dev)
+        d_segs = torch.from_numpy(segs.view(np.uint8).copy()).to(dev)
+        d_res = torch.zeros(max(n, 1) * 64, dtype=torch.uint8, device=dev)
+        d_used = torch.zeros(1, dtype=torch.int64, device=dev)
+        d_vscr = torch.zeros(max(self.scratch_bytes(n), 1), dtype=torch.uint8, device=dev)
+        self.validate_device(d_descs.data_ptr(), n, d_data.data_ptr(), d_res.data_ptr(), 0, 0,
+                             d_used.data_ptr(), d_vscr.data_ptr(), sh)
+        d_states = torch.zeros(max(ns, 1) * 48, dtype=torch.uint8, device=dev)
+        d_entries = torch.zeros(max(n, 1) * 16, dtype=torch.uint8, device=dev)
+        rc = self._lib.rpgpu_segment_index_device(self._ctx, d_descs.data_ptr(), d_res.data_ptr(),
+                                                  d_segs.data_ptr(), ns, d_states.data_ptr(),
+                                                  d_entries.data_ptr(), sh)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_segment_index_device: {rc} {self.last_error()}")
+        torch.cuda.synchronize(dev)
+        return dict(results=d_res.cpu().numpy().view(abi.RESULT_DTYPE)[:n].copy(),
+                    states=d_states.cpu().numpy().view(abi.SEGMENT_STATE_DTYPE)[:ns].copy(),
+                    entries=d_entries.cpu().numpy().view(abi.INDEX_ENTRY_DTYPE)[:n].copy())
+
     # -- synchronous scalar mirrors ---------------------------------------------------
     def uncompress(self, codec: int, data: bytes | np.ndarray, cap: int | None = None) -> tuple[int, bytes]:
         """compression::compressor::uncompress on the GPU: (verdict, bytes)."""

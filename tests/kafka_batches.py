@@ -36,7 +36,7 @@ def batch(records: list[bytes] | bytes, fmt: int = WIRE, base_offset: int = 0,
           record_count: int | None = None, attrs: int = 0, first_ts: int = 1_700_000_000_000,
           max_ts: int | None = None, pid: int = -1, pepoch: int = -1, bseq: int = -1,
           lod: int | None = None, leader_epoch: int = 0, magic: int = 2,
-          crc: int | None = None, batch_length: int | None = None) -> bytes:
+          crc: int | None = None, batch_length: int | None = None, btype: int = 1) -> bytes:
     body = records if isinstance(records, (bytes, bytearray)) else b"".join(records)
     rc = (len(records) if not isinstance(records, (bytes, bytearray)) else 0) \
         if record_count is None else record_count
@@ -50,7 +50,7 @@ def batch(records: list[bytes] | bytes, fmt: int = WIRE, base_offset: int = 0,
         bl = size - 12 if batch_length is None else batch_length
         hdr = struct.pack(">qiib", base_offset, bl, leader_epoch, magic) + struct.pack(">I", kcrc)
         return hdr + be40 + body
-    le = struct.pack("<iqbI", size, base_offset, 1, kcrc) + struct.pack("<hiqqqhii", *tail)
+    le = struct.pack("<iqbI", size, base_offset, btype, kcrc) + struct.pack("<hiqqqhii", *tail)
     return struct.pack("<I", orc.crc32c(le)) + le + body
 
 
