@@ -12,7 +12,8 @@ value)) over 4096 partitions per GPU.
 records x 1 KiB per GPU; one step = validation of the compressed batches,
 LZ4F decompression, the batch rewrite with fresh CRCs
 (maybe_decompress_batch_sync) and the record walk + index of the
-decompressed records.
+decompressed records.  --config c4 (configs[3]): the same with zstd bodies
+over 65,536 partitions.
 
 Multi-GPU: one process per GPU (torch.distributed, RCCL).  Partitions shard
 across GPUs (each rank owns its own partition range, weak scaling); the only
@@ -51,6 +52,13 @@ CONFIGS = {
                  "decompressed records",
         batches=1 << 18, partitions=4096, decompress=True,
         spec=dict(records_per_batch=64, key_len=16, value_len=999, codec=3)),
+    "c4": dict(
+        workload="C4: 262,144 zstd-compressed Kafka v2 batches per GPU (the reference's compressor: "
+                 "level 3, pledged content size), 64 records x 1 KiB (~64 KiB uncompressed), "
+                 "65,536 partitions; CRC32C + header CRC of the compressed batch, zstd decompression, "
+                 "batch rewrite with fresh CRCs, record walk + index of the decompressed records",
+        batches=1 << 18, partitions=65536, decompress=True,
+        spec=dict(records_per_batch=64, key_len=16, value_len=999, codec=4)),
     "c1": dict(
         workload="C1: 10,000 uncompressed Kafka v2 batches x 16,445 B (16 x 1 KiB records), "
                  "1 partition; CRC32C + header CRC + parse",
@@ -306,6 +314,7 @@ def main() -> int:
         import oracle.oracle as orc
 
         T = args.cpu_threads or nthreads
+        cfg_codec = cfg["spec"].get("codec", 0)
         sample_n = min(n, 2048)
         sdata, sdescs = engine.build_arena(spec, sample_n, first=first, nthreads=nthreads)
         sw = float(sdescs["length"].astype(np.float64).sum())
@@ -314,7 +323,7 @@ def main() -> int:
 
         def cpu_pass():
             r0, _, _ = orc.validate_arena(sdata, sdescs, nthreads=T, fast_crc=True)
-            return r0, orc.decompress_arena(sdata, sdescs, r0, caps, nthreads=T, out=obuf)
+            return r0, orc.decompress_arena(sdata, sdescs, r0, caps, codecs=(2, 3, 4), nthreads=T, out=obuf)
 
         cpu_pass()  # warm-up
         times, passes = [], 0
@@ -333,7 +342,8 @@ def main() -> int:
             "value": round(cpu_gbps, 2), "unit": "GB/s", "cores": T, "kind": "port",
             "sample": f"first {sample_n} batches of this workload ({sw / 1e9:.3f} GB compressed), "
                       f"median of {passes} passes: oracle/ C restatement (SSE4.2 CRC32C) + the "
-                      f"reference's LZ4F wrapper loop over liblz4 1.9.3 + rewrite + walk"}
+                      f"reference's {'LZ4F wrapper loop over liblz4 1.9.3' if cfg_codec == 3 else 'stream_zstd loop over libzstd 1.4.9'}"
+                      f" + rewrite + walk"}
         out["gpu_matches_oracle_on_sample"] = bool(same)
     elif rank == 0 and not args.no_cpu_baseline:
         import oracle.oracle as orc

@@ -24,9 +24,13 @@
 // Decoding is one lane per batch: an LZ4 or snappy stream is a chain of
 // dependent sequences, and with every batch of an arena in flight at once
 // (C3: 262,144 lanes, 16 waves per CU) the chip is filled with batches
-// rather than by splitting one stream.
+// rather than by splitting one stream.  zstd batches (codec 4) go to
+// zstd_kernel instead: one 64-lane workgroup per batch whose Huffman / FSE
+// tables (rpzstd::Ws, ~15 KB) sit in LDS; the frame is decoded by its first
+// lane (rpgpu_zstd.h).
 #include "rpgpu_device.h"  // before rpgpu_codec.h: HIP attributes
 #include "rpgpu_codec.h"
+#include "rpgpu_zstd.h"
 
 namespace rpgpu {
 
@@ -77,10 +81,11 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
     if (i < n) {
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
-        if (decomp_wanted(d, v) && (v.codec == 2 || v.codec == 3)) {
+        if (decomp_wanted(d, v) && (v.codec == 2 || v.codec == 3 || v.codec == 4)) {
             // verdict OK: kHeaderSize <= size_bytes <= descriptor length
             const uint64_t body = (uint64_t)(uint32_t)v.size_bytes - kHeaderSize;
-            const uint64_t bound = rpcodec::uncompress_bound(v.codec, data + d.offset + kHeaderSize, body);
+            const uint8_t* b = data + d.offset + kHeaderSize;
+            const uint64_t bound = v.codec == 4 ? rpzstd::bound(b, body) : rpcodec::uncompress_bound(v.codec, b, body);
             sz = (kHeaderSize + bound + rpcodec::kSlack + 15) & ~(uint64_t)15;
         }
     }
@@ -117,52 +122,34 @@ __device__ __forceinline__ void put_le(uint8_t* o, int off, uint64_t v, int nb) 
     for (int k = 0; k < nb; k++) o[off + k] = (uint8_t)(v >> (8 * k));
 }
 
-__global__ __launch_bounds__(256) void decomp_kernel(
-    const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
-    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
-    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
-    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
-    rpgpu_batch_desc* __restrict__ out_descs) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const rpgpu_batch_desc d = descs[i];
-    const rpgpu_batch_result v = vres[i];
-    const uint64_t off = block_base[i / kScanBlock] + local[i];
-    const uint64_t sz = slot[i];
-    int32_t verdict = RPGPU_V_SKIPPED;
-    uint64_t len = 0;
+// the batch's result, rewritten header and rewritten descriptor
+__device__ __forceinline__ void finish_batch(uint32_t i, const rpgpu_batch_desc& d, const rpgpu_batch_result& v,
+                                             uint64_t off, uint64_t sz, int32_t verdict, uint64_t len,
+                                             const uint8_t* __restrict__ data, uint8_t* __restrict__ out,
+                                             rpgpu_decomp_result* __restrict__ dres,
+                                             rpgpu_batch_desc* __restrict__ out_descs) {
     uint8_t ops = 0;
-    if (decomp_wanted(d, v)) {
-        if (sz == 0) {
-            verdict = RPGPU_V_DECOMP_UNSUPPORTED;  // gzip, zstd
-        } else if (off + sz > out_cap) {
-            verdict = RPGPU_V_DECOMP_OVERFLOW;  // caller's buffer smaller than the plan
-        } else {
-            const uint8_t* p = data + d.offset;
-            uint8_t* o = out + off;
-            verdict = rpcodec::uncompress(v.codec, p + kHeaderSize, (uint64_t)(uint32_t)v.size_bytes - kHeaderSize,
-                                          o + kHeaderSize, sz - kHeaderSize - rpcodec::kSlack, &len);
-            if (verdict == RPGPU_V_OK) {
-                // rewritten header in the on-disk layout (storage/parser.cc:40-80):
-                // codec bits removed, size_bytes = 61 + body (parser_utils.cc:61-64,124);
-                // crc / header_crc follow from the validation of the rewritten batch
-                const bool be = d.format == RPGPU_FMT_KAFKA_WIRE;
-                put_le(o, 0, 0, 4);
-                put_le(o, 4, kHeaderSize + len, 4);
-                put_le(o, 8, be ? hdr_field(p, 0, 8, true) : hdr_field(p, 8, 8, false), 8);
-                o[16] = be ? (uint8_t)1 : p[16];  // raft_data on produce
-                put_le(o, 17, 0, 4);
-                put_le(o, 21, hdr_field(p, 21, 2, be) & ~(uint64_t)7, 2);
-                put_le(o, 23, hdr_field(p, 23, 4, be), 4);
-                put_le(o, 27, hdr_field(p, 27, 8, be), 8);
-                put_le(o, 35, hdr_field(p, 35, 8, be), 8);
-                put_le(o, 43, hdr_field(p, 43, 8, be), 8);
-                put_le(o, 51, hdr_field(p, 51, 2, be), 2);
-                put_le(o, 53, hdr_field(p, 53, 4, be), 4);
-                put_le(o, 57, hdr_field(p, 57, 4, be), 4);
-                ops = RPGPU_OP_CRC | RPGPU_OP_HDRCRC | RPGPU_OP_RECRC | (d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX));
-            }
-        }
+    if (verdict == RPGPU_V_OK) {
+        // rewritten header in the on-disk layout (storage/parser.cc:40-80):
+        // codec bits removed, size_bytes = 61 + body (parser_utils.cc:61-64,124);
+        // crc / header_crc follow from the validation of the rewritten batch
+        const uint8_t* p = data + d.offset;
+        uint8_t* o = out + off;
+        const bool be = d.format == RPGPU_FMT_KAFKA_WIRE;
+        put_le(o, 0, 0, 4);
+        put_le(o, 4, kHeaderSize + len, 4);
+        put_le(o, 8, be ? hdr_field(p, 0, 8, true) : hdr_field(p, 8, 8, false), 8);
+        o[16] = be ? (uint8_t)1 : p[16];  // raft_data on produce
+        put_le(o, 17, 0, 4);
+        put_le(o, 21, hdr_field(p, 21, 2, be) & ~(uint64_t)7, 2);
+        put_le(o, 23, hdr_field(p, 23, 4, be), 4);
+        put_le(o, 27, hdr_field(p, 27, 8, be), 8);
+        put_le(o, 35, hdr_field(p, 35, 8, be), 8);
+        put_le(o, 43, hdr_field(p, 43, 8, be), 8);
+        put_le(o, 51, hdr_field(p, 51, 2, be), 2);
+        put_le(o, 53, hdr_field(p, 53, 4, be), 4);
+        put_le(o, 57, hdr_field(p, 57, 4, be), 4);
+        ops = RPGPU_OP_CRC | RPGPU_OP_HDRCRC | RPGPU_OP_RECRC | (d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX));
     }
     rpgpu_decomp_result r;
     r.verdict = verdict;
@@ -182,6 +169,64 @@ __global__ __launch_bounds__(256) void decomp_kernel(
     out_descs[i] = od;
 }
 
+__global__ __launch_bounds__(256) void decomp_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
+    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
+    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
+    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
+    rpgpu_batch_desc* __restrict__ out_descs) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const rpgpu_batch_desc d = descs[i];
+    const rpgpu_batch_result v = vres[i];
+    const bool want = decomp_wanted(d, v);
+    if (want && v.codec == 4) return;  // zstd_kernel
+    const uint64_t off = block_base[i / kScanBlock] + local[i];
+    const uint64_t sz = slot[i];
+    int32_t verdict = RPGPU_V_SKIPPED;
+    uint64_t len = 0;
+    if (want) {
+        if (sz == 0) {
+            verdict = RPGPU_V_DECOMP_UNSUPPORTED;  // gzip
+        } else if (off + sz > out_cap) {
+            verdict = RPGPU_V_DECOMP_OVERFLOW;  // caller's buffer smaller than the plan
+        } else {
+            const uint8_t* p = data + d.offset;
+            verdict = rpcodec::uncompress(v.codec, p + kHeaderSize, (uint64_t)(uint32_t)v.size_bytes - kHeaderSize,
+                                          out + off + kHeaderSize, sz - kHeaderSize - rpcodec::kSlack, &len);
+        }
+    }
+    finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
+}
+
+// zstd batches: one 64-lane workgroup per batch (grid-stride), tables in LDS
+constexpr uint32_t kZstdGrid = 2048;
+__global__ __launch_bounds__(64) void zstd_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
+    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
+    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
+    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
+    rpgpu_batch_desc* __restrict__ out_descs) {
+    __shared__ rpzstd::Ws ws;
+    if (threadIdx.x != 0) return;
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const rpgpu_batch_desc d = descs[i];
+        const rpgpu_batch_result v = vres[i];
+        if (!decomp_wanted(d, v) || v.codec != 4) continue;
+        const uint64_t off = block_base[i / kScanBlock] + local[i];
+        const uint64_t sz = slot[i];
+        int32_t verdict;
+        uint64_t len = 0;
+        if (off + sz > out_cap) {
+            verdict = RPGPU_V_DECOMP_OVERFLOW;
+        } else {
+            verdict = rpzstd::uncompress(data + d.offset + kHeaderSize, (uint64_t)(uint32_t)v.size_bytes - kHeaderSize,
+                                         out + off + kHeaderSize, sz - kHeaderSize - rpcodec::kSlack, &len, ws);
+        }
+        finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
+    }
+}
+
 // stores the CRCs the validation of the rewritten batches computed
 __global__ __launch_bounds__(256) void decomp_patch_kernel(const rpgpu_decomp_result* __restrict__ dres,
                                                            const rpgpu_batch_result* __restrict__ vres2, uint32_t n,
@@ -195,13 +240,16 @@ __global__ __launch_bounds__(256) void decomp_patch_kernel(const rpgpu_decomp_re
 
 // scalar mirror (rpgpu_uncompress): one lane
 __global__ void uncompress_bound_kernel(uint32_t codec, const uint8_t* in, uint64_t n, uint64_t* res) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) res[0] = rpcodec::uncompress_bound(codec, in, n);
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        res[0] = codec == 4 ? (n ? rpzstd::bound(in, n) : 0) : rpcodec::uncompress_bound(codec, in, n);
 }
 __global__ void uncompress_one_kernel(uint32_t codec, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap,
                                       uint64_t* res) {
+    __shared__ rpzstd::Ws ws;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         uint64_t len = 0;
-        res[1] = (uint64_t)(int64_t)rpcodec::uncompress(codec, in, n, out, cap, &len);
+        res[1] = (uint64_t)(int64_t)(codec == 4 ? rpzstd::uncompress(in, n, out, cap, &len, ws)
+                                                 : rpcodec::uncompress(codec, in, n, out, cap, &len));
         res[2] = len;
     }
 }
@@ -232,6 +280,9 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                                        out_cap, d_out_descs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    zstd_kernel<<<n < kZstdGrid ? n : kZstdGrid, 64, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
+                                                             p.block_sum, d_dres, d_out, out_cap, d_out_descs);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = launch_plan(d_out_descs, n, d_out, d_index_used, p.vscratch, s)) != hipSuccess) return e;
     if ((e = launch_run(d_out_descs, n, d_out, d_vres2, d_index, index_cap, p.vscratch, d_tables, grid, s, ov)) !=
         hipSuccess)

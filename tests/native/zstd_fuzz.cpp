@@ -1,0 +1,340 @@
+// zstd_fuzz.cpp — differential fuzz of the engine's zstd restatement
+// (redpanda_amd/csrc/rpgpu_zstd.h, compiled for the host) against the CPU
+// oracle (oracle/codec.c: the reference's stream_zstd::do_uncompress loop over
+// libzstd 1.4.9, the library the oracle links).  TEST INFRASTRUCTURE, built
+// and run by tests/test_zstd_fuzz.py; exits 1 at the first divergence.
+//
+// Component checks first, against libzstd 1.4.9's own exported internals:
+// FSE_readNCount on written-then-mutated headers, HUF_selectDecoder over the
+// (dstSize, cSrcSize) plane, and the static workspace budget.  Then whole
+// bodies: frames made by the library with varied level / window / checksum /
+// content-size / literal-mode settings, one-shot or flushed per fragment as
+// the reference's compressor does, concatenated frames and skippable frames,
+// then mutated (bit flips, byte overwrites, truncation, trailing junk,
+// rewritten header bytes).  Bytes past the input are garbage, as the next
+// batch of an arena would be.
+#define ZSTD_STATIC_LINKING_ONLY
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <zstd.h>
+
+#include <random>
+#include <vector>
+
+#include "rpgpu_zstd.h"
+
+extern "C" {
+int32_t orc_uncompress(int codec, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
+size_t FSE_readNCount(short* norm, unsigned* maxSV, unsigned* tableLog, const void* src, size_t n);
+unsigned FSE_isError(size_t code);
+size_t FSE_writeNCount(void* buf, size_t cap, const short* norm, unsigned maxSV, unsigned tableLog);
+size_t FSE_normalizeCount(short* norm, unsigned tableLog, const unsigned* count, size_t total, unsigned maxSV);
+uint32_t HUF_selectDecoder(size_t dstSize, size_t cSrcSize);
+}
+
+namespace {
+
+typedef std::vector<uint8_t> Bytes;
+std::mt19937_64 rng;
+uint64_t below(uint64_t n) { return n ? rng() % n : 0; }
+long n_cases = 0, n_ok = 0, n_rejected = 0;
+
+void fail(const char* what) {
+    fprintf(stderr, "FAIL: %s\n", what);
+    exit(1);
+}
+
+// ---------------------------------------------------------------- components
+void check_ncount(long rounds) {
+    for (long r = 0; r < rounds; r++) {
+        const unsigned maxSV = (const unsigned[]){255, 35, 52, 31, 7}[below(5)];
+        Bytes buf;
+        if (below(4) == 0) {
+            buf.resize(1 + below(40));
+            for (auto& b : buf) b = (uint8_t)rng();
+        } else {
+            // a valid header from a random histogram, then maybe mutated
+            unsigned count[256] = {0};
+            const unsigned used = 1 + (unsigned)below(maxSV + 1);
+            size_t total = 0;
+            for (unsigned s = 0; s < used; s++) {
+                count[s] = below(3) ? (unsigned)below(1 + below(2000)) : 0;
+                total += count[s];
+            }
+            if (total == 0) {
+                count[0] = 1;
+                total = 1;
+            }
+            unsigned last = used - 1;
+            while (last > 0 && count[last] == 0) last--;
+            const unsigned log = 5 + (unsigned)below(5);
+            short norm[256];
+            if (FSE_isError(FSE_normalizeCount(norm, log, count, total, last))) continue;
+            buf.resize(512);
+            const size_t w = FSE_writeNCount(buf.data(), buf.size(), norm, last, log);
+            if (FSE_isError(w)) continue;
+            buf.resize(w);
+            if (below(2)) {
+                const int m = 1 + (int)below(3);
+                for (int k = 0; k < m && !buf.empty(); k++) buf[below(buf.size())] ^= (uint8_t)(1u << below(8));
+            }
+            if (below(4) == 0 && buf.size() > 1) buf.resize(1 + below(buf.size() - 1));
+            if (below(4) == 0)
+                for (int k = 0, m = (int)below(6); k < m; k++) buf.push_back((uint8_t)rng());
+        }
+        Bytes padded = buf;
+        padded.resize(buf.size() + 16, 0xA5);
+        short ln[256];
+        unsigned lsv = maxSV, llog = 0;
+        const size_t lr = FSE_readNCount(ln, &lsv, &llog, padded.data(), buf.size());
+        int16_t en[256];
+        uint32_t esv = maxSV, elog = 0;
+        const int64_t er = rpzstd::read_ncount(en, &esv, &elog, padded.data(), buf.size());
+        const bool lerr = FSE_isError(lr) != 0;
+        if (lerr != (er < 0)) {
+            fprintf(stderr, "readNCount: lib %s engine %s (len %zu maxSV %u)\n", lerr ? "error" : "ok",
+                    er < 0 ? "error" : "ok", buf.size(), maxSV);
+            for (auto b : buf) fprintf(stderr, "%02x", b);
+            fprintf(stderr, "\n");
+            fail("FSE_readNCount acceptance");
+        }
+        if (!lerr) {
+            if ((int64_t)lr != er || lsv != esv || llog != elog) fail("FSE_readNCount header size / maxSV / log");
+            for (unsigned s = 0; s <= lsv; s++)
+                if (ln[s] != en[s]) fail("FSE_readNCount counts");
+        }
+    }
+}
+
+void check_select() {
+    for (size_t dst = 1; dst <= 128 * 1024; dst += 1 + below(700)) {
+        for (int k = 0; k < 24; k++) {
+            const size_t c = 1 + below(dst + dst / 4 + 16);
+            if ((HUF_selectDecoder(dst, c) != 0) != rpzstd::huf_select_x2(dst, c)) {
+                fprintf(stderr, "HUF_selectDecoder(%zu, %zu)\n", dst, c);
+                fail("HUF_selectDecoder");
+            }
+        }
+    }
+    const size_t budget = ZSTD_estimateDStreamSize(8u << 20) - ZSTD_estimateDCtxSize();
+    if (budget != rpzstd::kBudget) {
+        fprintf(stderr, "budget lib %zu engine %llu\n", budget, (unsigned long long)rpzstd::kBudget);
+        fail("workspace budget");
+    }
+}
+
+// ------------------------------------------------------------------ bodies
+Bytes payload(size_t n) {
+    Bytes v(n);
+    switch (below(6)) {
+    case 0: break;
+    case 1:
+        for (size_t i = 0; i < n;) {
+            const uint8_t b = (uint8_t)rng();
+            for (size_t r = 1 + below(300); r-- && i < n;) v[i++] = b;
+        }
+        break;
+    case 2: {
+        static const char* w[] = {"the ", "kafka ", "batch ", "record ", "offset ",
+                                  "redpanda ", "log ", "segment ", "a", "xyzzy "};
+        for (size_t i = 0; i < n;)
+            for (const char* s = w[below(10)]; *s && i < n;) v[i++] = (uint8_t)*s++;
+        break;
+    }
+    case 3: {
+        static const char an[] = "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789";
+        for (auto& b : v) b = (uint8_t)an[below(62)];
+        break;
+    }
+    case 4: {  // skewed bytes: small Huffman alphabets
+        const unsigned k = 2 + (unsigned)below(20);
+        for (auto& b : v) b = (uint8_t)('a' + below(1 + below(k)));
+        break;
+    }
+    default:
+        for (auto& b : v) b = (uint8_t)rng();
+    }
+    return v;
+}
+
+size_t rand_size() {
+    switch (below(6)) {
+    case 0: return below(24);
+    case 1: return below(300);
+    case 2: return below(5000);
+    case 3: return 60000 + below(10000);
+    case 4: return 120000 + below(200000);
+    default: return below(70000);
+    }
+}
+
+void ck(size_t r) {
+    if (ZSTD_isError(r)) {
+        fprintf(stderr, "zstd: %s\n", ZSTD_getErrorName(r));
+        exit(2);
+    }
+}
+
+Bytes lib_frame(const Bytes& src) {
+    ZSTD_CCtx* c = ZSTD_createCCtx();
+    const int levels[] = {-5, -1, 1, 2, 3, 3, 3, 5, 9, 19};
+    ck(ZSTD_CCtx_setParameter(c, ZSTD_c_compressionLevel, levels[below(10)]));
+    if (below(3) == 0) ck(ZSTD_CCtx_setParameter(c, ZSTD_c_windowLog, 10 + (int)below(12)));
+    ck(ZSTD_CCtx_setParameter(c, ZSTD_c_checksumFlag, below(4) == 0));
+    const bool content = below(4) != 0;
+    ck(ZSTD_CCtx_setParameter(c, ZSTD_c_contentSizeFlag, content));
+    if (below(4) == 0)
+        ck(ZSTD_CCtx_setParameter(c, ZSTD_c_literalCompressionMode,
+                                  below(2) ? ZSTD_lcm_uncompressed : ZSTD_lcm_huffman));
+    Bytes out(ZSTD_compressBound(src.size()) + 4096 + src.size() / 8);
+    ZSTD_outBuffer ob = {out.data(), out.size(), 0};
+    if (below(2)) {
+        // the reference's compressor: pledged size, ZSTD_e_flush per fragment
+        if (content) ck(ZSTD_CCtx_setPledgedSrcSize(c, src.size()));
+        size_t pos = 0;
+        while (pos < src.size()) {
+            const size_t frag = 1 + below(below(2) ? 4096 : 140000);
+            ZSTD_inBuffer ib = {src.data() + pos, frag < src.size() - pos ? frag : src.size() - pos, 0};
+            size_t r;
+            do {
+                r = ZSTD_compressStream2(c, &ob, &ib, ZSTD_e_flush);
+                ck(r);
+            } while (r > 0 || ib.pos < ib.size);
+            pos += ib.size;
+        }
+        ZSTD_inBuffer ib = {nullptr, 0, 0};
+        size_t r;
+        do {
+            r = ZSTD_compressStream2(c, &ob, &ib, ZSTD_e_end);
+            ck(r);
+        } while (r > 0);
+        out.resize(ob.pos);
+    } else {
+        const size_t r = ZSTD_compress2(c, out.data(), out.size(), src.data(), src.size());
+        ck(r);
+        out.resize(r);
+    }
+    ZSTD_freeCCtx(c);
+    return out;
+}
+
+void put32(Bytes& b, uint32_t v) {
+    for (int k = 0; k < 4; k++) b.push_back((uint8_t)(v >> (8 * k)));
+}
+
+Bytes body() {
+    Bytes b;
+    const int frames = below(5) == 0 ? 2 + (int)below(3) : 1;
+    for (int f = 0; f < frames; f++) {
+        if (below(8) == 0) {  // skippable frame
+            const size_t n = below(40);
+            put32(b, 0x184D2A50u + (uint32_t)below(16));
+            put32(b, (uint32_t)n);
+            for (size_t k = 0; k < n; k++) b.push_back((uint8_t)rng());
+        }
+        const Bytes fr = lib_frame(payload(f ? below(20000) : rand_size()));
+        b.insert(b.end(), fr.begin(), fr.end());
+    }
+    return b;
+}
+
+void mutate(Bytes& f) {
+    const int m = below(8);
+    if (m == 0 && !f.empty()) {
+        f[below(f.size())] ^= (uint8_t)(1u << below(8));
+    } else if (m == 1 && !f.empty()) {
+        for (int k = 0, c = 1 + (int)below(4); k < c; k++) f[below(f.size())] ^= (uint8_t)(1u << below(8));
+    } else if (m == 2 && !f.empty()) {
+        f[below(f.size())] = (uint8_t)rng();
+    } else if (m == 3) {
+        f.resize(below(f.size() + 1));
+    } else if (m == 4) {
+        for (int k = 0, c = 1 + (int)below(8); k < c; k++) f.push_back((uint8_t)rng());
+    } else if (m == 5 && f.size() > 6) {
+        // frame header descriptor / window byte
+        f[4 + below(2)] ^= (uint8_t)(1u << below(8));
+    } else if (m == 6 && f.size() > 20) {
+        // bytes just after the header: block header / literals header
+        const size_t at = 5 + below(12);
+        f[at] ^= (uint8_t)(1u << below(8));
+    }
+}
+
+void compare(const Bytes& in) {
+    n_cases++;
+    Bytes padded = in;
+    padded.resize(in.size() + 64);
+    for (size_t k = in.size(); k < padded.size(); k++) padded[k] = (uint8_t)rng();
+    const uint8_t* ip = padded.data();
+    const uint64_t cap = rpzstd::bound(ip, in.size());
+    Bytes eout(cap + 1);
+    static rpzstd::Ws ws;
+    uint64_t elen = 0;
+    const int32_t ev = rpzstd::uncompress(ip, in.size(), eout.data(), cap, &elen, ws);
+    static Bytes oout(96u << 20);
+    size_t olen = 0;
+    const int32_t ov = orc_uncompress(4, ip, in.size(), oout.data(), oout.size(), &olen);
+    if (ov == 34) return;  // oracle sink too small: not comparable
+    bool same = ev == ov;
+    if (same && ev == 0) same = elen == olen && !memcmp(eout.data(), oout.data(), olen);
+    if (!same) {
+        fprintf(stderr, "case %ld: engine v=%d len=%llu (bound %llu), oracle v=%d len=%zu, input %zu bytes\n", n_cases,
+                ev, (unsigned long long)elen, (unsigned long long)cap, ov, olen, in.size());
+        if (ev == 0 && ov == 0) {
+            size_t k = 0;
+            while (k < elen && k < olen && eout[k] == oout[k]) k++;
+            fprintf(stderr, "first differing byte %zu\n", k);
+        }
+        FILE* fp = fopen("zstd_fuzz_fail.bin", "wb");
+        if (fp) {
+            fwrite(in.data(), 1, in.size(), fp);
+            fclose(fp);
+        }
+        exit(1);
+    }
+    if (ev == 0) {
+        n_ok++;
+    } else {
+        n_rejected++;
+    }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    long cases = 2000;
+    uint64_t seed = 1;
+    const char* replay = nullptr;
+    for (int a = 1; a + 1 < argc; a += 2) {
+        if (!strcmp(argv[a], "--cases")) cases = atol(argv[a + 1]);
+        if (!strcmp(argv[a], "--seed")) seed = strtoull(argv[a + 1], nullptr, 0);
+        if (!strcmp(argv[a], "--replay")) replay = argv[a + 1];
+    }
+    rng.seed(seed);
+    if (replay) {
+        FILE* fp = fopen(replay, "rb");
+        if (!fp) return 2;
+        Bytes in;
+        int c;
+        while ((c = fgetc(fp)) != EOF) in.push_back((uint8_t)c);
+        fclose(fp);
+        compare(in);
+        printf("replay: engine == oracle\n");
+        return 0;
+    }
+    check_select();
+    check_ncount(cases * 4);
+    for (long i = 0; i < cases; i++) {
+        Bytes b = body();
+        compare(b);
+        for (int k = 0, m = 1 + (int)below(4); k < m; k++) {
+            Bytes c = b;
+            mutate(c);
+            if (below(3) == 0) mutate(c);
+            compare(c);
+        }
+    }
+    printf("zstd fuzz: %ld cases, %ld decoded, %ld rejected: engine == oracle\n", n_cases, n_ok, n_rejected);
+    return 0;
+}

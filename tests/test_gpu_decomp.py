@@ -1,12 +1,11 @@
 """GPU parity of the decompress path (rpgpu_decomp_plan_device /
 rpgpu_decomp_run_device and the rpgpu_uncompress scalar mirror) against the
 oracle: compression::compressor::uncompress (compression/compression.cc:35-55)
-over liblz4 / snappy through the reference's wrapper loops, the batch rewrite
+over liblz4 / snappy / libzstd through the reference's wrapper loops, the batch rewrite
 of maybe_decompress_batch_sync (storage/parser_utils.cc:52-68,122-128) and the
 record walk of the rewritten batches.  Compared per batch: decompress verdict,
 decoded length, the rewritten batch's bytes (header with fresh CRCs + body),
-its validation result and its index entries.  zstd batches must report
-RPGPU_V_DECOMP_UNSUPPORTED (not decoded on the GPU yet)."""
+its validation result and its index entries."""
 import os
 import sys
 
@@ -30,7 +29,7 @@ def compare(got, data, descs):
     wres, _, _ = orc.validate_arena(data, descs)
     assert np.array_equal(res.view(np.uint8), wres.view(np.uint8)), "validation results differ"
     caps = np.where(dres["out_cap"] > 0, dres["out_cap"].astype(np.int64) - 61 - 128, 0).astype(np.uint64)
-    want = orc.decompress_arena(data, descs, wres, caps)
+    want = orc.decompress_arena(data, descs, wres, caps, codecs=(2, 3, 4))
     bad = np.nonzero(dres["verdict"] != want["verdicts"])[0]
     assert bad.size == 0, (f"decompress verdicts differ at {bad[:8]}: gpu {dres['verdict'][bad[:8]]} "
                            f"oracle {want['verdicts'][bad[:8]]}")
@@ -64,7 +63,7 @@ def records(rng, n, key_len, value_len, text):
     return out
 
 
-@pytest.mark.parametrize("codec", [2, 3])
+@pytest.mark.parametrize("codec", [2, 3, 4])
 @pytest.mark.parametrize("fmt", [WIRE, DISK])
 def test_generated_arenas(eng, codec, fmt):
     """Builder arenas (rpgen: the reference's compressor settings), text and alnum payloads."""
@@ -91,8 +90,10 @@ def test_mixed_codecs_corrupted(eng):
     got = eng.decompress_arena(data, descs)
     compare(got, data, descs)
     v = got["dres"]["verdict"]
-    assert (v == abi.V_DECOMP_UNSUPPORTED).sum() > 0  # zstd
+    assert (v == abi.V_DECOMP_UNSUPPORTED).sum() == 0
     assert (v == abi.V_OK).sum() > 10
+    codec = got["dres"]["codec"]
+    assert ((v == abi.V_OK) & (codec == 4)).sum() > 0
 
 
 def mutated_bodies(rng, codec, n):
@@ -115,6 +116,8 @@ def mutated_bodies(rng, codec, n):
             comp += bytes(rng.integers(0, 256, int(rng.integers(1, 9)), dtype=np.uint8))
         elif kind == 4 and codec == 3 and len(comp) > 11:
             comp = comp[:-4]  # no end mark: truncated right after the last block
+        elif kind == 4 and codec == 4:
+            comp += orc.compress(4, body[: len(body) // 2])  # a second frame
         elif kind == 5 and len(comp) > 20:
             k = int(rng.integers(16, len(comp)))
             comp[k] = 0xFF
@@ -122,7 +125,7 @@ def mutated_bodies(rng, codec, n):
     return out
 
 
-@pytest.mark.parametrize("codec", [2, 3])
+@pytest.mark.parametrize("codec", [2, 3, 4])
 @pytest.mark.parametrize("fmt", [WIRE, DISK])
 def test_mutated_payloads(eng, codec, fmt):
     rng = np.random.default_rng(100 + codec * 2 + fmt)
@@ -132,10 +135,11 @@ def test_mutated_payloads(eng, codec, fmt):
 
 
 def test_large_bodies(eng):
-    """~1 MiB bodies: many 64 KiB LZ4 blocks, several 128 KiB snappy-java chunks."""
+    """~1 MiB bodies: many 64 KiB LZ4 blocks, several 128 KiB snappy-java chunks,
+    zstd frames larger than the 64 KiB staging buffer (streamed block by block)."""
     rng = np.random.default_rng(7)
     bs = []
-    for codec in (2, 3, 3, 2):
+    for codec in (2, 3, 3, 2, 4, 4):
         recs = records(rng, 900, 8, 1100, text=codec == 3)
         bs.append(batch(orc.compress(codec, b"".join(recs)), fmt=WIRE, record_count=len(recs), attrs=codec))
     data, descs = arena(bs, fmt=WIRE, ops=OPS)
@@ -145,10 +149,11 @@ def test_large_bodies(eng):
 def test_uncompress_scalar_mirror(eng):
     rng = np.random.default_rng(3)
     cases = []
-    for codec in (2, 3):
+    for codec in (2, 3, 4):
         for c, _ in mutated_bodies(rng, codec, 40):
             cases.append((codec, c))
-    cases += [(3, b""), (2, b""), (0, b"abc"), (3, b"\x04\x22\x4d"), (2, b"\x00")]
+    cases += [(3, b""), (2, b""), (4, b""), (0, b"abc"), (3, b"\x04\x22\x4d"), (2, b"\x00"),
+              (4, b"\x28\xb5\x2f\xfd"), (4, b"\x28\xb5\x2f\xfd\x00"), (4, b"\x50\x2a\x4d\x18\x00\x00\x00\x00")]
     for codec, c in cases:
         gv, gout = eng.uncompress(codec, c, cap=1 << 21)
         ov, oout = orc.uncompress(codec, c, cap=1 << 21)
