@@ -98,6 +98,150 @@ RPC_HD uint32_t hb32(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }  /
 RPC_HD uint32_t le24(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16); }
 RPC_HD uint64_t lomask(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
 
+// ------------------------------------------------------------ exact copies
+// Unlike rpcodec's wild copies these write exactly n bytes: the Huffman
+// literals sit in the slot tail right behind the output, so no store may run
+// past the end of a sequence.
+RPC_HD void st_part(uint8_t* p, uint64_t lo, uint64_t hi, uint64_t n) {  // n < 16 bytes of lo|hi
+    if (n & 8) {
+        __builtin_memcpy(p, &lo, 8);
+        p += 8;
+        lo = hi;
+    }
+    if (n & 4) {
+        const uint32_t v = (uint32_t)lo;
+        __builtin_memcpy(p, &v, 4);
+        p += 4;
+        lo >>= 32;
+    }
+    if (n & 2) {
+        const uint16_t v = (uint16_t)lo;
+        __builtin_memcpy(p, &v, 2);
+        p += 2;
+        lo >>= 16;
+    }
+    if (n & 1) *p = (uint8_t)lo;
+}
+// literals: src >= dst or disjoint (a forward copy whose 16-byte chunks are
+// each read before written; the last, overlapping chunk is read up front)
+RPC_HD void copy_lits(uint8_t* dst, const uint8_t* src, uint64_t n) {
+    using rpcodec::B16;
+    if (n < 16) {
+        if (n) st_part(dst, le64(src), le64(src + 8), n);
+        return;
+    }
+    B16 last;
+    rpcodec::ld16(last, src + n - 16);
+    uint64_t i = 0;
+    for (; i + 64 <= n; i += 64) {
+        B16 a, b, c, d;
+        rpcodec::ld16(a, src + i);
+        rpcodec::ld16(b, src + i + 16);
+        rpcodec::ld16(c, src + i + 32);
+        rpcodec::ld16(d, src + i + 48);
+        rpcodec::st16(dst + i, a);
+        rpcodec::st16(dst + i + 16, b);
+        rpcodec::st16(dst + i + 32, c);
+        rpcodec::st16(dst + i + 48, d);
+    }
+    for (; i + 16 <= n; i += 16) {
+        B16 a;
+        rpcodec::ld16(a, src + i);
+        rpcodec::st16(dst + i, a);
+    }
+    rpcodec::st16(dst + n - 16, last);
+}
+// match: dst[i] = dst[i - off] for i in [0, n), off >= 1
+RPC_HD void copy_seq_match(uint8_t* dst, uint64_t off, uint64_t n) {
+    using rpcodec::B16;
+    if (off >= 16) {
+        if (n < 16) {
+            st_part(dst, le64(dst - off), le64(dst - off + 8), n);
+            return;
+        }
+        uint64_t i = 0;
+        if (off >= 64) {
+            for (; i + 64 <= n; i += 64) {
+                B16 a, b, c, d;
+                rpcodec::ld16(a, dst - off + i);
+                rpcodec::ld16(b, dst - off + i + 16);
+                rpcodec::ld16(c, dst - off + i + 32);
+                rpcodec::ld16(d, dst - off + i + 48);
+                rpcodec::st16(dst + i, a);
+                rpcodec::st16(dst + i + 16, b);
+                rpcodec::st16(dst + i + 32, c);
+                rpcodec::st16(dst + i + 48, d);
+            }
+        }
+        for (; i + 16 <= n; i += 16) {
+            B16 a;
+            rpcodec::ld16(a, dst - off + i);
+            rpcodec::st16(dst + i, a);
+        }
+        if (i < n) {  // the last 16 bytes, whose source is written by now
+            B16 a;
+            rpcodec::ld16(a, dst + n - 16 - off);
+            rpcodec::st16(dst + n - 16, a);
+        }
+        return;
+    }
+    // period-off pattern in a 16-byte register, stored a whole number of periods apart
+    const uint8_t* s = dst - off;
+    uint64_t lo = le64(s), hi = le64(s + 8);
+    if (off <= 8) {
+        if (off < 8) lo &= (1ull << (8 * off)) - 1;
+        hi = 0;
+    } else {
+        hi &= (1ull << (8 * (off - 8))) - 1;
+    }
+    for (uint64_t w = off; w < 16; w *= 2) {
+        const uint64_t sh = 8 * w;
+        if (sh < 64) {
+            hi |= (hi << sh) | (lo >> (64 - sh));
+            lo |= lo << sh;
+        } else {
+            hi |= lo << (sh - 64);
+        }
+    }
+    const uint64_t step = off * (16 / off);
+    B16 p;
+    p.w[0] = (uint32_t)lo;
+    p.w[1] = (uint32_t)(lo >> 32);
+    p.w[2] = (uint32_t)hi;
+    p.w[3] = (uint32_t)(hi >> 32);
+    uint64_t i = 0;
+    for (; i + 16 <= n; i += step) rpcodec::st16(dst + i, p);
+    if (i < n) st_part(dst + i, lo, hi, n - i);
+}
+
+RPC_HD void fill_bytes(uint8_t* dst, uint8_t v, uint64_t n) {
+    const uint64_t x = 0x0101010101010101ull * v;
+    rpcodec::B16 p;
+    p.w[0] = p.w[1] = p.w[2] = p.w[3] = (uint32_t)x;
+    uint64_t i = 0;
+    for (; i + 16 <= n; i += 16) rpcodec::st16(dst + i, p);
+    if (i < n) st_part(dst + i, x, x, n - i);
+}
+
+// Huffman output: bytes gathered 8 at a time into one store
+struct ByteOut {
+    uint8_t* p;
+    uint64_t acc;
+    uint32_t n;
+};
+RPC_HD void bo_put(ByteOut& o, uint32_t v) {
+    o.acc |= (uint64_t)(v & 0xFF) << (8 * o.n);
+    if (++o.n == 8) {
+        __builtin_memcpy(o.p, &o.acc, 8);
+        o.p += 8;
+        o.acc = 0;
+        o.n = 0;
+    }
+}
+RPC_HD void bo_flush(ByteOut& o) {
+    if (o.n) st_part(o.p, o.acc, 0, o.n);
+}
+
 // HUF_selectDecoder: 1 -> the double-symbol (X2) decoder
 RPC_HD bool huf_select_x2(uint64_t dst, uint64_t csrc) {
     const uint32_t q = csrc >= dst ? 15u : (uint32_t)(csrc * 16 / dst);
@@ -113,6 +257,8 @@ RPC_HD bool huf_select_x2(uint64_t dst, uint64_t csrc) {
 struct Ws {
     uint16_t huf[1u << kHufMaxLog];  // X1 table: symbol | nbBits << 8
     uint32_t ll[512], ml[512], of[256];  // sequence tables: state << 16 | nbBits << 8 | symbol
+    uint32_t llx[512], mlx[512];     // per state: baseline | extra bits << 24 (ZSTD_seqSymbol's
+                                     // baseValue / nbAdditionalBits: no dependent lookup per field)
     uint32_t wt[64];                 // HUF weight FSE table: state << 16 | nbBits << 8 | symbol
     int16_t norm[256];
     uint16_t next[256];
@@ -129,10 +275,15 @@ struct Ws {
 // past the start libzstd keeps reading its drained container (the first
 // <= 8 bytes, `c0`) with bitsConsumed > 64 and shift counts masked to 6 bits,
 // which BIT_readBits and BIT_readBitsFast do differently: both are restated.
+// The stream is immutable, so reads are served from a cached 64-bit window
+// (`win` = stream bits [8*wb, 8*wb + 64)): one 8-byte load per ~7 bytes
+// consumed instead of a dependent load per field.
 struct Bits {
     const uint8_t* s;
     int64_t pos;
     uint64_t c0;
+    int64_t wb;  // window base, bytes
+    uint64_t win;
 };
 
 RPC_HD bool bits_init(Bits& b, const uint8_t* s, uint64_t n) {  // BIT_initDStream
@@ -148,12 +299,20 @@ RPC_HD bool bits_init(Bits& b, const uint8_t* s, uint64_t n) {  // BIT_initDStre
         for (uint64_t i = 0; i < n; i++) c |= (uint64_t)s[i] << (8 * i);
     }
     b.c0 = c;
+    b.wb = -64;  // empty window
+    b.win = 0;
     return true;
 }
-// bits [lo, lo + n) of the stream, lo >= 0, n <= 57 (reads up to 7 bytes past
-// the stream: the arena tail pad covers the last one)
-RPC_HD uint64_t bits_at(const Bits& b, int64_t lo, uint32_t n) {
-    return (le64(b.s + ((uint64_t)lo >> 3)) >> (lo & 7)) & lomask(n);
+// bits [lo, lo + n) of the stream, lo >= 0, n <= 57 (the window may reach up
+// to 7 bytes past the stream: the arena tail pad covers it)
+RPC_HD uint64_t bits_at(Bits& b, int64_t lo, uint32_t n) {
+    if (lo < 8 * b.wb || lo + (int64_t)n > 8 * b.wb + 64) {
+        int64_t wb = ((lo + (int64_t)n + 7) >> 3) - 8;  // window top at or just above lo + n
+        if (wb < 0) wb = 0;
+        b.wb = wb;
+        b.win = le64(b.s + wb);
+    }
+    return (b.win >> (lo - 8 * b.wb)) & lomask(n);
 }
 RPC_HD uint64_t read_bits(Bits& b, uint32_t n) {  // BIT_readBits (lookBits + skip)
     uint64_t v;
@@ -182,7 +341,7 @@ RPC_HD uint64_t read_bits_fast(Bits& b, uint32_t n) {  // BIT_readBitsFast, n >=
 // remain, and at exactly 0 bits left (bitsConsumed == 64, shift 0) it is the
 // container's top bits again, which HUF_decodeLastSymbolX2 decodes a symbol
 // from without consuming anything.
-RPC_HD uint32_t peek_fast(const Bits& b, int64_t pos, uint32_t n) {
+RPC_HD uint32_t peek_fast(Bits& b, int64_t pos, uint32_t n) {
     if (pos >= (int64_t)n) return (uint32_t)bits_at(b, pos - n, n);
     const uint32_t bc = (uint32_t)(64 - pos);
     return (uint32_t)((b.c0 << (bc & 63u)) >> ((64u - n) & 63u));
@@ -414,45 +573,81 @@ RPC_HD int64_t huf_read_table(Ws& w, const uint8_t* in, uint64_t n) {
 // same symbols pairwise from a 12-bit table and, for a final unpaired symbol,
 // skips the whole pair entry clamped at the stream start
 // (HUF_decodeLastSymbolX2).  Success = the stream consumed exactly.
-RPC_HD bool huf_stream(const Ws& w, const uint8_t* src, uint64_t len, uint8_t* out, uint64_t nsym, uint64_t nwrite) {
+// A stream is a state advanced one symbol per step, so that the four streams
+// of a 4-stream literals section advance interleaved (four independent
+// dependency chains in flight, as HUF_decompress4X does).
+struct HufS {
     Bits b;
-    if (!bits_init(b, src, len)) return RPZ_FAIL(false);
+    ByteOut o;
+    uint64_t i, nsym, nwrite;
+    bool second;  // X2: this symbol is the second half of a pair entry
+    bool live;    // symbols left
+    bool ok;
+};
+RPC_HD bool huf_begin(HufS& h, const uint8_t* src, uint64_t len, uint8_t* out, uint64_t nsym, uint64_t nwrite) {
+    h.o = ByteOut{out, 0, 0};
+    h.i = 0;
+    h.nsym = nsym;
+    h.nwrite = nwrite;
+    h.second = false;
+    h.ok = bits_init(h.b, src, len);
+    h.live = h.ok && nsym > 0;
+    return h.ok;
+}
+RPC_HD void huf_end(HufS& h) {
+    bo_flush(h.o);
+    h.live = false;
+#ifdef RPZ_TRACE
+    if (h.ok && h.b.pos != 0)
+        fprintf(stderr, "huf_stream: nsym %llu end pos %lld\n", (unsigned long long)h.nsym, (long long)h.b.pos);
+#endif
+    h.ok = h.ok && h.b.pos == 0;
+}
+RPC_HD void huf_step(const Ws& w, HufS& h, uint32_t L, bool x2) {
+    if (!h.live) return;
+    if (h.b.pos < 0) {
+        h.ok = false;
+        huf_end(h);
+        return;
+    }
+    const uint64_t i = h.i;
+    if (x2 && !h.second) {
+        // the X2 entry: the 12-bit window holds this code and, if it fits, the next
+        const uint32_t v = peek_fast(h.b, h.b.pos, kHufMaxLog);
+        const uint32_t e = w.huf[v >> (kHufMaxLog - L)];
+        const uint32_t nb = e >> 8;
+        const uint32_t e2 = w.huf[((v << nb) & ((1u << kHufMaxLog) - 1)) >> (kHufMaxLog - L)];
+        const bool pair = nb + (e2 >> 8) <= kHufMaxLog;
+        if (i < h.nwrite) bo_put(h.o, e);
+        if (i + 1 == h.nsym) {  // HUF_decodeLastSymbolX2
+            if (!pair) {
+                h.b.pos -= nb;
+            } else if (h.b.pos > 0) {
+                h.b.pos -= (int64_t)(nb + (e2 >> 8));
+                if (h.b.pos < 0) h.b.pos = 0;
+            }
+            huf_end(h);
+            return;
+        }
+        h.second = pair;
+        h.b.pos -= nb;
+    } else {
+        const uint32_t e = w.huf[peek_fast(h.b, h.b.pos, L)];
+        if (i < h.nwrite) bo_put(h.o, e);
+        h.second = false;
+        h.b.pos -= e >> 8;
+    }
+    h.i = i + 1;
+    if (h.i == h.nsym) huf_end(h);
+}
+RPC_HD bool huf_stream(const Ws& w, const uint8_t* src, uint64_t len, uint8_t* out, uint64_t nsym, uint64_t nwrite) {
+    HufS h;
+    if (!huf_begin(h, src, len, out, nsym, nwrite)) return RPZ_FAIL(false);
+    if (!h.live) huf_end(h);
     const uint32_t L = w.huf_log;
     const bool x2 = w.huf_x2 != 0;
-    bool second = false;  // X2: this symbol is the second half of a pair entry
-    for (uint64_t i = 0; i < nsym; i++) {
-        if (b.pos < 0) return RPZ_FAIL(false);
-        if (x2 && !second) {
-            // the X2 entry: the 12-bit window holds this code and, if it fits, the next
-            const uint32_t v = peek_fast(b, b.pos, kHufMaxLog);
-            const uint32_t e = w.huf[v >> (kHufMaxLog - L)];
-            const uint32_t nb = e >> 8;
-            const uint32_t e2 = w.huf[((v << nb) & ((1u << kHufMaxLog) - 1)) >> (kHufMaxLog - L)];
-            const bool pair = nb + (e2 >> 8) <= kHufMaxLog;
-            if (i < nwrite) out[i] = (uint8_t)e;
-            if (i + 1 == nsym) {  // HUF_decodeLastSymbolX2
-                if (!pair) {
-                    b.pos -= nb;
-                } else if (b.pos > 0) {
-                    b.pos -= (int64_t)(nb + (e2 >> 8));
-                    if (b.pos < 0) b.pos = 0;
-                }
-                break;
-            }
-            second = pair;
-            b.pos -= nb;
-        } else {
-            const uint32_t e = w.huf[peek_fast(b, b.pos, L)];
-            if (i < nwrite) out[i] = (uint8_t)e;
-            second = false;
-            b.pos -= e >> 8;
-        }
-    }
-#ifdef RPZ_TRACE
-    if (b.pos != 0) fprintf(stderr, "huf_stream: nsym %llu len %llu x2 %d log %u end pos %lld\n", (unsigned long long)nsym,
-                            (unsigned long long)len, (int)x2, L, (long long)b.pos);
-#endif
-    return b.pos == 0;
+    while (h.live) huf_step(w, h, L, x2);
+    return h.ok;
 }
 
 // ---------------------------------------------------------------- blocks
@@ -489,7 +684,7 @@ RPC_HD int64_t literals(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint
         if (size > tail - op) return -2;
         uint8_t* d = out + tail - size;
         const uint8_t v = in[hs];
-        for (uint64_t i = 0; i < size; i++) d[i] = v;
+        fill_bytes(d, v, size);
         lit.p = d;
         lit.n = size;
         return (int64_t)(hs + 1);
@@ -540,22 +735,40 @@ RPC_HD int64_t literals(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint
         const uint64_t l4 = slen - (l1 + l2 + l3 + 6);
         if (l4 > slen) return RPZ_FAIL(-1);
         const uint64_t seg = (size + 3) / 4;
-        const uint64_t lens[4] = {l1, l2, l3, l4};
-        const uint8_t* s = src + 6;
         // every stream must initialise before any decodes (BIT_initDStream x4)
-        for (int k = 0; k < 4; k++) {
+        {
             Bits t;
-            if (!bits_init(t, s, lens[k])) return RPZ_FAIL(-1);
-            s += lens[k];
+            if (!bits_init(t, src + 6, l1) || !bits_init(t, src + 6 + l1, l2) ||
+                !bits_init(t, src + 6 + l1 + l2, l3) || !bits_init(t, src + 6 + l1 + l2 + l3, l4))
+                return RPZ_FAIL(-1);
         }
-        s = src + 6;
-        for (uint64_t k = 0; k < 4; k++) {
-            const uint64_t at = k * seg;
-            const uint64_t nsym = k < 3 ? seg : (size > 3 * seg ? size - 3 * seg : 0);
-            const uint64_t nwrite = at >= size ? 0 : (size - at < nsym ? size - at : nsym);
-            if (!huf_stream(w, s, lens[k], d + (at < size ? at : 0), nsym, nwrite)) return RPZ_FAIL(-1);
-            s += lens[k];
+        // the four streams, interleaved one symbol each per step
+        const uint32_t L = w.huf_log;
+        const bool x2 = w.huf_x2 != 0;
+        HufS h0, h1, h2, h3;
+        const uint64_t n3 = size > 3 * seg ? size - 3 * seg : 0;
+        // stream k: symbols [k*seg, ...), writes clipped to the section size
+        const uint64_t at1 = seg, at2 = 2 * seg, at3 = 3 * seg;
+        const uint64_t w0 = size < seg ? size : seg;
+        const uint64_t w1 = at1 >= size ? 0 : (size - at1 < seg ? size - at1 : seg);
+        const uint64_t w2 = at2 >= size ? 0 : (size - at2 < seg ? size - at2 : seg);
+        const uint64_t w3 = at3 >= size ? 0 : (size - at3 < n3 ? size - at3 : n3);
+        const uint8_t* s0 = src + 6;
+        huf_begin(h0, s0, l1, d, seg, w0);
+        huf_begin(h1, s0 + l1, l2, d + (at1 < size ? at1 : 0), seg, w1);
+        huf_begin(h2, s0 + l1 + l2, l3, d + (at2 < size ? at2 : 0), seg, w2);
+        huf_begin(h3, s0 + l1 + l2 + l3, l4, d + (at3 < size ? at3 : 0), n3, w3);
+        if (!h0.live) huf_end(h0);
+        if (!h1.live) huf_end(h1);
+        if (!h2.live) huf_end(h2);
+        if (!h3.live) huf_end(h3);
+        while (h0.live | h1.live | h2.live | h3.live) {
+            huf_step(w, h0, L, x2);
+            huf_step(w, h1, L, x2);
+            huf_step(w, h2, L, x2);
+            huf_step(w, h3, L, x2);
         }
+        if (!(h0.ok && h1.ok && h2.ok && h3.ok)) return RPZ_FAIL(-1);
     }
     w.lit_entropy = 1;
     lit.p = d;
@@ -570,7 +783,23 @@ RPC_HD void build_default(uint32_t* t, uint16_t* next, int16_t* norm, const int8
 }
 
 // ZSTD_buildSeqTable for one of LL / OF / ML.  Returns bytes or -1.
+RPC_HD void seq_extra(Ws& w, uint32_t which) {
+    if (which == 1) return;
+    const uint32_t* t = which == 0 ? w.ll : w.ml;
+    uint32_t* x = which == 0 ? w.llx : w.mlx;
+    const uint32_t size = 1u << (which == 0 ? w.ll_log : w.ml_log);
+    for (uint32_t u = 0; u < size; u++) {
+        const uint32_t c = t[u] & 0xFF;
+        x[u] = which == 0 ? (kLLBase[c] | ((uint32_t)kLLBits[c] << 24)) : (kMLBase[c] | ((uint32_t)kMLBits[c] << 24));
+    }
+}
+RPC_HD int64_t seq_table_impl(Ws& w, uint32_t mode, uint32_t which, const uint8_t* in, uint64_t n);
 RPC_HD int64_t seq_table(Ws& w, uint32_t mode, uint32_t which, const uint8_t* in, uint64_t n) {
+    const int64_t h = seq_table_impl(w, mode, which, in, n);
+    if (h >= 0 && mode != 3) seq_extra(w, which);
+    return h;
+}
+RPC_HD int64_t seq_table_impl(Ws& w, uint32_t mode, uint32_t which, const uint8_t* in, uint64_t n) {
     uint32_t* t = which == 0 ? w.ll : (which == 1 ? w.of : w.ml);
     uint8_t& log = which == 0 ? w.ll_log : (which == 1 ? w.of_log : w.ml_log);
     const uint32_t max = which == 0 ? 35u : (which == 1 ? 31u : 52u);
@@ -657,9 +886,10 @@ RPC_HD int64_t block(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_
         uint32_t sML = (uint32_t)read_bits(b, w.ml_log);
         for (uint32_t k = 0; k < nbSeq; k++) {
             const uint32_t eLL = w.ll[sLL], eML = w.ml[sML], eOF = w.of[sOF];
-            const uint32_t cLL = eLL & 0xFF, cML = eML & 0xFF, cOF = eOF & 0xFF;
-            const uint32_t llBase = kLLBase[cLL], mlBase = kMLBase[cML];
-            const uint32_t llBits = kLLBits[cLL], mlBits = kMLBits[cML], ofBits = cOF;
+            const uint32_t xLL = w.llx[sLL], xML = w.mlx[sML];
+            const uint32_t cOF = eOF & 0xFF;
+            const uint32_t llBase = xLL & 0xFFFFFF, mlBase = xML & 0xFFFFFF;
+            const uint32_t llBits = xLL >> 24, mlBits = xML >> 24, ofBits = cOF;
             const uint32_t ofBase = cOF == 0 ? 0u : (cOF == 1 ? 1u : (1u << cOF) - 3u);
             uint64_t offset;
             if (ofBits > 1) {
@@ -698,11 +928,9 @@ RPC_HD int64_t block(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_
             if (ll > (uint64_t)(lend - lp)) return RPZ_FAIL(-1);
             const uint64_t lit_end = o + ll;
             if (offset > lit_end - fstart) return RPZ_FAIL(-1);
-            for (uint64_t i = 0; i < ll; i++) out[o + i] = lp[i];
+            copy_lits(out + o, lp, ll);
             lp += ll;
-            uint8_t* d = out + lit_end;
-            const uint8_t* m = d - offset;
-            for (uint64_t i = 0; i < ml; i++) d[i] = m[i];
+            copy_seq_match(out + lit_end, offset, ml);
             o = lit_end + ml;
         }
         if (b.pos > 0) return RPZ_FAIL(-1);  // BIT_reloadDStream < BIT_DStream_completed
@@ -712,7 +940,7 @@ RPC_HD int64_t block(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_
     }
     const uint64_t last = (uint64_t)(lend - lp);
     if (last > oend - o) return RPZ_FAIL(-1);
-    for (uint64_t i = 0; i < last; i++) out[o + i] = lp[i];
+    copy_lits(out + o, lp, last);
     o += last;
     return (int64_t)(o - op);
 }
@@ -915,13 +1143,13 @@ RPC_HD int32_t uncompress_impl(const uint8_t* in, uint64_t n, uint8_t* out, uint
                 } else if (type == 0) {
                     if (size > fend - T) return RPZ_FAIL(V_ERROR);
                     if (T + size > cap) return V_OVERFLOW;
-                    for (uint64_t i = 0; i < size; i++) out[T + i] = f[ip + i];
+                    copy_lits(out + T, f + ip, size);
                     r = (int64_t)size;
                     ip += size;
                 } else {
                     if (size > fend - T) return RPZ_FAIL(V_ERROR);
                     if (T + size > cap) return V_OVERFLOW;
-                    for (uint64_t i = 0; i < size; i++) out[T + i] = f[ip];
+                    fill_bytes(out + T, f[ip], size);
                     r = (int64_t)size;
                     ip += 1;
                 }
@@ -966,7 +1194,7 @@ RPC_HD int32_t uncompress_impl(const uint8_t* in, uint64_t n, uint8_t* out, uint
                     if (take == 0) break;
                     if (take > room_ring) return RPZ_FAIL(V_ERROR);
                     if (T + take > cap) return V_OVERFLOW;
-                    for (uint64_t i = 0; i < take; i++) out[T + i] = f[ip + i];
+                    copy_lits(out + T, f + ip, take);
                     ip += take;
                     T += take;
                     decoded += take;
@@ -978,7 +1206,7 @@ RPC_HD int32_t uncompress_impl(const uint8_t* in, uint64_t n, uint8_t* out, uint
                     if (size > room_ring) return RPZ_FAIL(V_ERROR);
                     if (size > h.bsm) return RPZ_FAIL(V_ERROR);
                     if (T + size > cap) return V_OVERFLOW;
-                    for (uint64_t i = 0; i < size; i++) out[T + i] = f[ip];
+                    fill_bytes(out + T, f[ip], size);
                     ip += 1;
                     r = size;
                     T += r;
