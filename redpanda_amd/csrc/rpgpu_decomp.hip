@@ -200,7 +200,6 @@ __global__ __launch_bounds__(256) void decomp_kernel(
 }
 
 // zstd batches: one 64-lane workgroup per batch (grid-stride), tables in LDS
-constexpr uint32_t kZstdGrid = 2048;
 __global__ __launch_bounds__(64) void zstd_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
     const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
@@ -208,11 +207,27 @@ __global__ __launch_bounds__(64) void zstd_kernel(
     rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
     rpgpu_batch_desc* __restrict__ out_descs) {
     __shared__ rpzstd::Ws ws;
+#if RPGPU_ZSTD_PREFETCH
+    const uint32_t t = threadIdx.x;
+#else
     if (threadIdx.x != 0) return;
+#endif
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
         if (!decomp_wanted(d, v) || v.codec != 4) continue;
+#if RPGPU_ZSTD_PREFETCH
+        {
+            // the whole wave touches every 128-byte line of the frame once, so the
+            // serial decoder's window loads hit L2 instead of going to HBM
+            const uint8_t* b = data + d.offset;
+            const uint64_t nb = (uint64_t)(uint32_t)v.size_bytes;
+            uint32_t acc = 0;
+            for (uint64_t k = (uint64_t)t * 128; k < nb; k += 64 * 128) acc ^= b[k];
+            asm volatile("" ::"v"(acc));
+        }
+        if (t != 0) continue;
+#endif
         const uint64_t off = block_base[i / kScanBlock] + local[i];
         const uint64_t sz = slot[i];
         int32_t verdict;
@@ -280,7 +295,18 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                                        out_cap, d_out_descs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    zstd_kernel<<<n < kZstdGrid ? n : kZstdGrid, 64, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
+    // one decoder per LDS-resident workgroup slot: the decode is latency-bound,
+    // so every slot the LDS footprint allows is filled (10 per CU on gfx950)
+    static const uint32_t zgrid = [] {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, zstd_kernel, 64, 0) != hipSuccess || cus <= 0 ||
+            per_cu <= 0)
+            return 2048u;
+        return (uint32_t)(cus * per_cu);
+    }();
+    zstd_kernel<<<n < zgrid ? n : zgrid, 64, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
                                                              p.block_sum, d_dres, d_out, out_cap, d_out_descs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = launch_plan(d_out_descs, n, d_out, d_index_used, p.vscratch, s)) != hipSuccess) return e;
