@@ -25,9 +25,8 @@
 // dependent sequences, and with every batch of an arena in flight at once
 // (C3: 262,144 lanes, 16 waves per CU) the chip is filled with batches
 // rather than by splitting one stream.  zstd batches (codec 4) go to
-// zstd_kernel instead: one 64-lane workgroup per batch whose Huffman / FSE
-// tables (rpzstd::Ws, ~15 KB) sit in LDS; the frame is decoded by its first
-// lane (rpgpu_zstd.h).
+// zstd_kernel instead: also one lane per batch, each with its own Huffman /
+// FSE workspace (rpzstd::Ws, ~19 KB) in HBM (rpgpu_zstd.h).
 #include "rpgpu_device.h"  // before rpgpu_codec.h: HIP attributes
 #include "rpgpu_codec.h"
 #include "rpgpu_zstd.h"
@@ -44,15 +43,20 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
 size_t validate_scratch_bytes(uint32_t n);
 
 namespace {
-// scratch: slot[n] u64 | local[n] u64 | block_sum[nb] u64 | validate scratch
+// zstd decoders in flight at once (one lane each), and so per-lane workspaces
+constexpr uint32_t kZstdLanes = 131072;
+uint32_t zstd_lanes(uint32_t n) { return n < kZstdLanes ? n : kZstdLanes; }
+// scratch: slot[n] u64 | local[n] u64 | block_sum[nb] u64 | validate scratch | zstd Ws[lanes]
 struct Parts {
     uint64_t *slot, *local, *block_sum;
     void* vscratch;
+    rpzstd::Ws* zws;
 };
 size_t parts_head(uint32_t n) {
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
     return ((size_t)n * 16 + nb * 8 + 255) & ~(size_t)255;
 }
+size_t zws_offset(uint32_t n) { return (parts_head(n) + validate_scratch_bytes(n) + 255) & ~(size_t)255; }
 Parts parts(void* p, uint32_t n) {
     uint8_t* b = static_cast<uint8_t*>(p);
     Parts s;
@@ -60,11 +64,12 @@ Parts parts(void* p, uint32_t n) {
     s.local = s.slot + n;
     s.block_sum = s.local + n;
     s.vscratch = b + parts_head(n);
+    s.zws = reinterpret_cast<rpzstd::Ws*>(b + zws_offset(n));
     return s;
 }
 }  // namespace
 
-size_t decomp_scratch_bytes(uint32_t n) { return parts_head(n) + validate_scratch_bytes(n); }
+size_t decomp_scratch_bytes(uint32_t n) { return zws_offset(n) + (size_t)zstd_lanes(n) * sizeof(rpzstd::Ws); }
 
 __device__ __forceinline__ bool decomp_wanted(const rpgpu_batch_desc& d, const rpgpu_batch_result& v) {
     return (d.ops & RPGPU_OP_DECOMP) && v.verdict == RPGPU_V_OK && v.codec != 0;
@@ -199,35 +204,24 @@ __global__ __launch_bounds__(256) void decomp_kernel(
     finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
 }
 
-// zstd batches: one 64-lane workgroup per batch (grid-stride), tables in LDS
-__global__ __launch_bounds__(64) void zstd_kernel(
+// zstd batches: one lane per batch (grid-stride over kZstdLanes lanes), each
+// with its own workspace (Huffman / FSE tables) in HBM.  The decode is a chain
+// of dependent loads per symbol and per sequence; what hides that latency is
+// the number of frames in flight, so tables live where every lane can have
+// its own rather than in LDS (~19 KB per frame caps LDS at 8 frames per CU).
+__global__ __launch_bounds__(256) void zstd_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
     const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
     rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
-    rpgpu_batch_desc* __restrict__ out_descs) {
-    __shared__ rpzstd::Ws ws;
-#if RPGPU_ZSTD_PREFETCH
-    const uint32_t t = threadIdx.x;
-#else
-    if (threadIdx.x != 0) return;
-#endif
-    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    rpgpu_batch_desc* __restrict__ out_descs, rpzstd::Ws* __restrict__ wsbuf) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lanes = gridDim.x * blockDim.x;
+    rpzstd::Ws& ws = wsbuf[g];
+    for (uint32_t i = g; i < n; i += lanes) {
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
         if (!decomp_wanted(d, v) || v.codec != 4) continue;
-#if RPGPU_ZSTD_PREFETCH
-        {
-            // the whole wave touches every 128-byte line of the frame once, so the
-            // serial decoder's window loads hit L2 instead of going to HBM
-            const uint8_t* b = data + d.offset;
-            const uint64_t nb = (uint64_t)(uint32_t)v.size_bytes;
-            uint32_t acc = 0;
-            for (uint64_t k = (uint64_t)t * 128; k < nb; k += 64 * 128) acc ^= b[k];
-            asm volatile("" ::"v"(acc));
-        }
-        if (t != 0) continue;
-#endif
         const uint64_t off = block_base[i / kScanBlock] + local[i];
         const uint64_t sz = slot[i];
         int32_t verdict;
@@ -295,19 +289,9 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                                        out_cap, d_out_descs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    // one decoder per LDS-resident workgroup slot: the decode is latency-bound,
-    // so every slot the LDS footprint allows is filled (10 per CU on gfx950)
-    static const uint32_t zgrid = [] {
-        int dev = 0, cus = 0, per_cu = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, zstd_kernel, 64, 0) != hipSuccess || cus <= 0 ||
-            per_cu <= 0)
-            return 2048u;
-        return (uint32_t)(cus * per_cu);
-    }();
-    zstd_kernel<<<n < zgrid ? n : zgrid, 64, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
-                                                             p.block_sum, d_dres, d_out, out_cap, d_out_descs);
+    const uint32_t zl = zstd_lanes(n);
+    zstd_kernel<<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
+                                                 out_cap, d_out_descs, p.zws);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = launch_plan(d_out_descs, n, d_out, d_index_used, p.vscratch, s)) != hipSuccess) return e;
     if ((e = launch_run(d_out_descs, n, d_out, d_vres2, d_index, index_cap, p.vscratch, d_tables, grid, s, ov)) !=

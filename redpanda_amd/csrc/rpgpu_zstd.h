@@ -53,6 +53,14 @@
 #define RPZ_FAIL(v) (v)
 #endif
 
+// Once-per-block functions are kept out of line on the device: inlined at
+// every call site the kernel's code outgrew the instruction cache.
+#if defined(__HIPCC__) && !defined(RPZ_INLINE_ALL)
+#define RPZ_COLD __host__ __device__ __attribute__((noinline))
+#else
+#define RPZ_COLD RPC_HD
+#endif
+
 namespace rpzstd {
 
 using rpcodec::le16;
@@ -267,7 +275,15 @@ struct Ws {
     uint64_t rep[3];
     uint8_t ll_log, ml_log, of_log, huf_log;
     uint8_t huf_x2, lit_entropy, fse_entropy, pad;
+#if RPZ_PROF
+    uint64_t t_lit, t_seq, n_seq, n_lit;  // diagnostics build: clock64 per phase
+#endif
 };
+#if RPZ_PROF && defined(__HIP_DEVICE_COMPILE__)
+#define RPZ_CLK() ((uint64_t)clock64())
+#else
+#define RPZ_CLK() ((uint64_t)0)
+#endif
 
 // --------------------------------------------------------------- bit reader
 // BIT_DStream_t read backwards.  `pos` = bits not yet read below the read
@@ -658,7 +674,7 @@ struct Lit {
 
 // ZSTD_decodeLiteralsBlock.  Huffman / RLE literals go to out[tail - n, tail).
 // Returns section bytes, -1 on error, -2 when the tail would reach `op`.
-RPC_HD int64_t literals(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t op, uint64_t tail, Lit& lit) {
+RPZ_COLD int64_t literals(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t op, uint64_t tail, Lit& lit) {
     if (n < 3) return RPZ_FAIL(-1);  // MIN_CBLOCK_SIZE
     const uint32_t type = in[0] & 3, lh = (in[0] >> 2) & 3;
     if (type == 0 || type == 1) {  // raw / RLE
@@ -834,12 +850,20 @@ RPC_HD int64_t seq_table_impl(Ws& w, uint32_t mode, uint32_t which, const uint8_
 // ZSTD_decompressBlock_internal for one compressed block: output at out[op..),
 // history from out[fstart..), at most `cap` bytes; literals may use the slot
 // tail [.., tail).  Returns bytes produced, -1 error, -2 slot exceeded.
-RPC_HD int64_t block(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t fstart, uint64_t op, uint64_t cap,
+RPZ_COLD int64_t block(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t fstart, uint64_t op, uint64_t cap,
                      uint64_t tail) {
     if (n >= kBlockMax) return RPZ_FAIL(-1);
     Lit lit;
+#if RPZ_PROF
+    const uint64_t c0 = RPZ_CLK();
+#endif
     const int64_t lh = literals(w, in, n, out, op, tail, lit);
     if (lh < 0) return lh;
+#if RPZ_PROF
+    const uint64_t c1 = RPZ_CLK();
+    w.t_lit += c1 - c0;
+    w.n_lit += lit.n;
+#endif
     const uint8_t* ip = in + lh;
     uint64_t rem = n - (uint64_t)lh;
     // ZSTD_decodeSeqHeaders
@@ -933,6 +957,10 @@ RPC_HD int64_t block(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_
             copy_seq_match(out + lit_end, offset, ml);
             o = lit_end + ml;
         }
+#if RPZ_PROF
+        w.t_seq += RPZ_CLK() - c1;
+        w.n_seq += nbSeq;
+#endif
         if (b.pos > 0) return RPZ_FAIL(-1);  // BIT_reloadDStream < BIT_DStream_completed
         w.rep[0] = (uint32_t)rep0;
         w.rep[1] = (uint32_t)rep1;
