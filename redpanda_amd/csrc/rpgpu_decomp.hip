@@ -209,7 +209,10 @@ __global__ __launch_bounds__(256) void decomp_kernel(
 // of dependent loads per symbol and per sequence; what hides that latency is
 // the number of frames in flight, so tables live where every lane can have
 // its own rather than in LDS (~19 KB per frame caps LDS at 8 frames per CU).
-__global__ __launch_bounds__(256) void zstd_kernel(
+#ifndef RPZ_MIN_WAVES
+#define RPZ_MIN_WAVES 1
+#endif
+__global__ __launch_bounds__(256, RPZ_MIN_WAVES) void zstd_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
     const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
