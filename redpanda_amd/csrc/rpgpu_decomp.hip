@@ -44,7 +44,10 @@ size_t validate_scratch_bytes(uint32_t n);
 
 namespace {
 // zstd decoders in flight at once (one lane each), and so per-lane workspaces
-constexpr uint32_t kZstdLanes = 131072;
+#ifndef RPZ_LANES
+#define RPZ_LANES 131072  // 2 waves per SIMD at the kernel's VGPR count
+#endif
+constexpr uint32_t kZstdLanes = RPZ_LANES;
 uint32_t zstd_lanes(uint32_t n) { return n < kZstdLanes ? n : kZstdLanes; }
 // scratch: slot[n] u64 | local[n] u64 | block_sum[nb] u64 | validate scratch | zstd Ws[lanes]
 struct Parts {
