@@ -37,8 +37,8 @@
 // bytes) by libzstd.  Valid frames decode identically.
 //
 // Serial per frame: the same code runs on the host in the differential fuzz
-// (tests/native/zstd_fuzz.cpp) and on the device in one lane of a wave whose
-// tables sit in LDS (rpgpu_decomp.hip).  Huffman literals are decoded into the
+// (tests/native/zstd_fuzz.cpp) and on the device in one lane per batch, each
+// lane with its own workspace in HBM (rpgpu_decomp.hip).  Huffman literals are decoded into the
 // tail of the batch's output slot and read back from there by the sequences
 // (the output never overtakes them).
 #ifndef RPGPU_ZSTD_H
@@ -261,7 +261,7 @@ RPC_HD bool huf_select_x2(uint64_t dst, uint64_t csrc) {
 }
 
 // ------------------------------------------------------------- workspace
-// Per-frame decoder state (LDS on the device): ~15 KB.
+// Per-frame decoder state (per lane in HBM on the device; LDS for the scalar mirror): ~19 KB.
 struct Ws {
     uint16_t huf[1u << kHufMaxLog];  // X1 table: symbol | nbBits << 8
     uint32_t ll[512], ml[512], of[256];  // sequence tables: state << 16 | nbBits << 8 | symbol
