@@ -292,14 +292,15 @@ struct Ws {
 // <= 8 bytes, `c0`) with bitsConsumed > 64 and shift counts masked to 6 bits,
 // which BIT_readBits and BIT_readBitsFast do differently: both are restated.
 // The stream is immutable, so reads are served from a cached 64-bit window
-// (`win` = stream bits [8*wb, 8*wb + 64)): one 8-byte load per ~7 bytes
-// consumed instead of a dependent load per field.
+// (`win`, `win_hi` = stream bits [8*wb, 8*wb + 128)): one 16-byte load per
+// ~15 bytes consumed instead of a dependent load per field.
 struct Bits {
     const uint8_t* s;
     int64_t pos;
     uint64_t c0;
     int64_t wb;  // window base, bytes
-    uint64_t win;
+    uint64_t win, win_hi;
+    int64_t wbits;  // window width: 128 bits, 64 for streams under 16 bytes
 };
 
 RPC_HD bool bits_init(Bits& b, const uint8_t* s, uint64_t n) {  // BIT_initDStream
@@ -316,19 +317,29 @@ RPC_HD bool bits_init(Bits& b, const uint8_t* s, uint64_t n) {  // BIT_initDStre
     }
     b.c0 = c;
     b.wb = -64;  // empty window
-    b.win = 0;
+    b.win = b.win_hi = 0;
+    b.wbits = n >= 16 ? 128 : 64;
     return true;
 }
 // bits [lo, lo + n) of the stream, lo >= 0, n <= 57 (the window may reach up
 // to 7 bytes past the stream: the arena tail pad covers it)
 RPC_HD uint64_t bits_at(Bits& b, int64_t lo, uint32_t n) {
-    if (lo < 8 * b.wb || lo + (int64_t)n > 8 * b.wb + 64) {
-        int64_t wb = ((lo + (int64_t)n + 7) >> 3) - 8;  // window top at or just above lo + n
+    if (lo < 8 * b.wb || lo + (int64_t)n > 8 * b.wb + b.wbits) {
+        // window top at or just above lo + n; a 16-byte window stays inside a
+        // stream of >= 16 bytes (top <= stream end), an 8-byte one may reach 7 past
+        int64_t wb = ((lo + (int64_t)n + 7) >> 3) - (b.wbits >> 3);
         if (wb < 0) wb = 0;
         b.wb = wb;
         b.win = le64(b.s + wb);
+        b.win_hi = b.wbits == 128 ? le64(b.s + wb + 8) : 0;
     }
-    return (b.win >> (lo - 8 * b.wb)) & lomask(n);
+    const int64_t off = lo - 8 * b.wb;
+    uint64_t v;
+    if (off < 64)
+        v = off ? (b.win >> off) | (b.win_hi << (64 - off)) : b.win;
+    else
+        v = b.win_hi >> (off - 64);
+    return v & lomask(n);
 }
 RPC_HD uint64_t read_bits(Bits& b, uint32_t n) {  // BIT_readBits (lookBits + skip)
     uint64_t v;
