@@ -224,6 +224,11 @@ __global__ __launch_bounds__(256, RPZ_MIN_WAVES) void zstd_kernel(
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lanes = gridDim.x * blockDim.x;
     rpzstd::Ws& ws = wsbuf[g];
+#if RPZ_PROF
+    const uint64_t k0 = RPZ_CLK();
+    uint32_t nb_done = 0;
+    ws.t_lit = ws.t_seq = ws.n_seq = ws.n_lit = 0;
+#endif
     for (uint32_t i = g; i < n; i += lanes) {
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
@@ -239,7 +244,16 @@ __global__ __launch_bounds__(256, RPZ_MIN_WAVES) void zstd_kernel(
                                          out + off + kHeaderSize, sz - kHeaderSize - rpcodec::kSlack, &len, ws);
         }
         finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
+#if RPZ_PROF
+        nb_done++;
+#endif
     }
+#if RPZ_PROF
+    if (g < 4 || g == lanes - 1)  // diagnostics build: phase clocks of a few lanes
+        printf("RPZ_PROF lane=%u batches=%u total=%llu lit=%llu seq=%llu n_lit=%llu n_seq=%llu\n", g, nb_done,
+               (unsigned long long)(RPZ_CLK() - k0), (unsigned long long)ws.t_lit, (unsigned long long)ws.t_seq,
+               (unsigned long long)ws.n_lit, (unsigned long long)ws.n_seq);
+#endif
 }
 
 // stores the CRCs the validation of the rewritten batches computed
