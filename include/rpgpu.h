@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RPGPU_ABI_VERSION 1
+#define RPGPU_ABI_VERSION 2
 #define RPGPU_ARENA_TAIL_PAD 64
 #define RPGPU_HEADER_SIZE 61 /* model/record.h:527-540 */
 
@@ -85,7 +85,11 @@ enum rpgpu_verdict {
     RPGPU_V_FALLOCATED_ZERO = 22,  /* parser_errc::fallocated_file_read_zero_bytes_for_header */
     /* decompression (compression/compression.cc:35-55 and the codec wrappers) */
     RPGPU_V_DECOMP_ERROR = 30,     /* codec library error -> runtime_error         */
-    RPGPU_V_DECOMP_BAD_ALLOC = 31, /* zstd window > workspace -> std::bad_alloc   */
+    /* 31 is reserved (RPGPU_V_DECOMP_BAD_ALLOC in ABI v1, never produced): the
+     * reference's zstd bad_alloc branch is dead code (stream_zstd.cc:29-36
+     * compares the size_t return with the error enum), so a frame window the
+     * 8 MiB workspace cannot hold is RPGPU_V_DECOMP_ERROR like every other
+     * zstd error. */
     RPGPU_V_LZ4_TRAILING = 32,     /* unconsumed input after LZ4 frame end        */
     RPGPU_V_DECOMP_UNSUPPORTED = 33,/* codec not implemented on this engine (gzip) */
     RPGPU_V_DECOMP_OVERFLOW = 34,  /* decompressed size exceeds the output slot   */
@@ -98,11 +102,20 @@ enum rpgpu_verdict {
                                       validated OK, or not compressed        */
 };
 
-/* Produce-path mapping of verdicts to Kafka error codes
- * (kafka/protocol/errors.h:29,47,227). */
+/* Kafka error codes of the produce path (kafka/protocol/errors.h:22,29,47,227). */
+#define RPGPU_KAFKA_ERR_UNKNOWN_SERVER_ERROR (-1)
 #define RPGPU_KAFKA_ERR_NONE 0
 #define RPGPU_KAFKA_ERR_CORRUPT_MESSAGE 2
+#define RPGPU_KAFKA_ERR_MESSAGE_TOO_LARGE 10
 #define RPGPU_KAFKA_ERR_INVALID_RECORD 87
+
+/* rpgpu_batch_desc.flags */
+enum rpgpu_desc_flag {
+    /* the partition's records field was null on the wire (decoder::
+     * read_nullable_iobuf, kafka/protocol/wire.h:152-159): no bytes are read,
+     * the verdict is RPGPU_V_NULL_RECORDS (produce.cc:440-449) */
+    RPGPU_DESC_NULL_RECORDS = 1u << 0,
+};
 
 /* ---- descriptors and results ------------------------------------------ */
 typedef struct rpgpu_batch_desc {
@@ -111,7 +124,7 @@ typedef struct rpgpu_batch_desc {
     uint32_t partition; /* topic-partition id (sharding key)                 */
     uint8_t format;     /* enum rpgpu_format                                 */
     uint8_t ops;        /* enum rpgpu_op bitmask                             */
-    uint16_t flags;     /* reserved, 0                                       */
+    uint16_t flags;     /* enum rpgpu_desc_flag bitmask                      */
     uint32_t reserved;  /* reserved, 0                                       */
 } rpgpu_batch_desc;     /* 24 bytes */
 
@@ -209,6 +222,27 @@ int32_t rpgpu_submit(rpgpu_ctx* ctx, const rpgpu_batch_desc* descs, uint32_t n,
 int32_t rpgpu_poll(rpgpu_ctx* ctx, rpgpu_ticket ticket);
 /* Blocks until the ticket completes. */
 int32_t rpgpu_wait(rpgpu_ctx* ctx, rpgpu_ticket ticket);
+/* A non-blocking eventfd (EFD_NONBLOCK | EFD_CLOEXEC) owned by the context:
+ * it becomes readable whenever a stage of a submission completes, so a
+ * Seastar reactor awaits it with a readable() future on the fd (the
+ * ssx::thread_worker pattern, ssx/thread_worker.h:97-174) instead of
+ * blocking in rpgpu_wait; on readiness it reads the counter and calls
+ * rpgpu_poll.  -1 if the context has none. */
+int rpgpu_eventfd(rpgpu_ctx* ctx);
+
+/* ---- produce-handler glue ---------------------------------------------------
+ * The per-partition error code produce_handler would answer for a batch with
+ * this validation result (kafka/server/handlers/produce.cc:440-489, and the
+ * batch_max_bytes check of produce_topic_partition, produce.cc:317-324;
+ * batch_max_bytes 0 = no limit).  Verdicts whose reference behaviour is an
+ * exception escaping the request decoder (HDR_TRUNC_THROW, BAD_CODEC_THROW,
+ * BODY_TRUNC_THROW) map to RPGPU_KAFKA_ERR_UNKNOWN_SERVER_ERROR; TOO_SMALL
+ * and BAD_MAGIC, whose reference flags are uninitialised (kafka_batch_adapter.h:65-66),
+ * map to RPGPU_KAFKA_ERR_INVALID_RECORD.  Pure host function. */
+int32_t rpgpu_kafka_error_code(const rpgpu_batch_result* r, uint32_t batch_max_bytes);
+/* The same over a device result array: d_codes[i] (int32) for d_results[i]. */
+int32_t rpgpu_kafka_error_codes_device(rpgpu_ctx* ctx, const rpgpu_batch_result* d_results, uint32_t n,
+                                       uint32_t batch_max_bytes, int32_t* d_codes, void* hip_stream);
 
 /* Device-resident entry point: every pointer is device memory, the work is
  * enqueued on `hip_stream` (a hipStream_t; NULL = the context stream) and the
@@ -248,21 +282,23 @@ int32_t rpgpu_crc32c_ranges_device(rpgpu_ctx* ctx, const uint8_t* d_data,
  *   crc::crc32c::extend                 hashing/crc32c.h:21-43
  *   model::internal_header_only_crc     model/record_utils.cc:34-55
  *   model::crc_record_batch             model/record_utils.cc:82-87
- */
-uint32_t rpgpu_crc32c_extend(rpgpu_ctx* ctx, uint32_t crc, const void* p, size_t n);
-uint32_t rpgpu_internal_header_only_crc(rpgpu_ctx* ctx, const rpgpu_rp_header* h);
+ * Status return (RPGPU_OK or < 0); the value goes to *out. */
+int32_t rpgpu_crc32c_extend(rpgpu_ctx* ctx, uint32_t crc, const void* p, size_t n, uint32_t* out);
+int32_t rpgpu_internal_header_only_crc(rpgpu_ctx* ctx, const rpgpu_rp_header* h, uint32_t* out);
 int32_t rpgpu_crc_record_batch(rpgpu_ctx* ctx, const rpgpu_rp_header* h,
-                               const void* body, size_t n);
+                               const void* body, size_t n, int32_t* out);
 
 /* ---- decompression (storage read path) ---------------------------------
  * Replaces, per compressed batch,
  *   compression::compressor::uncompress            compression/compression.cc:35-55
  *     lz4_frame_compressor::uncompress             compression/internal/lz4_frame_compressor.cc:160-278
+ *     stream_zstd::do_uncompress                   compression/stream_zstd.cc:198-223
  *     snappy_java_compressor::uncompress           compression/internal/snappy_java_compressor.cc:76-110
+ *     gzip_compressor::uncompress                  compression/internal/gzip_compressor.cc:177-229
  *   storage::internal::maybe_decompress_batch_sync storage/parser_utils.cc:52-68,122-128
  * and walks / indexes the records of the decompressed batch
- * (model/record.h:668-691).  zstd and gzip are not decoded yet:
- * RPGPU_V_DECOMP_UNSUPPORTED.
+ * (model/record.h:668-691).  Every codec is decoded for one contiguous
+ * (single-fragment) body; see DESIGN.md §4 for the fragmented-iobuf case.
  *
  * A batch is decompressed when its descriptor has RPGPU_OP_DECOMP, its
  * validation verdict (d_results of rpgpu_run_device / rpgpu_validate_device

@@ -216,7 +216,7 @@ static int32_t walk_records(const uint8_t* body, size_t n, int32_t record_count,
  * Every fully parsed record consumes >= 2 bytes (a length varint byte and the
  * attributes byte), so the walk can never emit more. */
 uint32_t orc_index_cap(const rpgpu_batch_desc* d, const uint8_t* data) {
-    if (!(d->ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX))) return 0;
+    if (!(d->ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX)) || (d->flags & RPGPU_DESC_NULL_RECORDS)) return 0;
     const uint8_t* p = data + d->offset;
     uint64_t len = d->length;
     if (len < RPGPU_HEADER_SIZE) return 0;
@@ -419,7 +419,11 @@ static void* arena_worker(void* arg) {
         uint32_t cap = (uint32_t)(j->first[i + 1] - j->first[i]);
         rpgpu_record_index* e = j->idx ? j->idx + j->first[i] : NULL;
         if (!e) cap = 0;
-        if (d->format == RPGPU_FMT_KAFKA_WIRE)
+        if (d->flags & RPGPU_DESC_NULL_RECORDS) {
+            /* produce.cc:440-449: null records field -> invalid_record */
+            memset(&j->res[i], 0, sizeof(j->res[i]));
+            j->res[i].verdict = RPGPU_V_NULL_RECORDS;
+        } else if (d->format == RPGPU_FMT_KAFKA_WIRE)
             orc_kafka_adapt(j->data + d->offset, d->length, d->ops, &j->res[i], e, cap);
         else
             orc_disk_batch(j->data + d->offset, d->length, d->ops, &j->res[i], e, cap);

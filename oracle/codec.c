@@ -139,9 +139,12 @@ static int32_t zstd_uncompress(const uint8_t* src, size_t n, struct sink* s) {
             sink_append(s, obuf, sizeof(obuf));
             out.size = sizeof(obuf);
             out.pos = 0;
-        } else if (ZSTD_isError(err)) { /* throw_if_error, :29-41 */
-            if (ZSTD_getErrorCode(err) == ZSTD_error_memory_allocation)
-                return RPGPU_V_DECOMP_BAD_ALLOC;
+        } else if (ZSTD_isError(err)) {
+            /* throw_if_error -> throw_zstd_err, :29-41.  Its bad_alloc branch
+             * compares the raw size_t return, (size_t)-ZSTD_error_memory_allocation,
+             * with the enum value ZSTD_error_memory_allocation (64): never
+             * equal, so every zstd error -- a window the static workspace
+             * cannot hold included -- throws std::runtime_error. */
             return RPGPU_V_DECOMP_ERROR;
         }
     }

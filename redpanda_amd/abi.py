@@ -41,7 +41,6 @@ V_HDR_CRC_MISMATCH = 20
 V_STREAM_SHORT = 21
 V_FALLOCATED_ZERO = 22
 V_DECOMP_ERROR = 30
-V_DECOMP_BAD_ALLOC = 31
 V_LZ4_TRAILING = 32
 V_DECOMP_UNSUPPORTED = 33
 V_DECOMP_OVERFLOW = 34
@@ -53,7 +52,17 @@ VERDICT_NAMES = {v: k for k, v in globals().items() if k.startswith("V_") and is
 
 RPGPU_OK = 0
 RPGPU_PENDING = 1
+RPGPU_EINVAL = -1
 RPGPU_ECAPACITY = -4
+ABI_VERSION = 2
+
+DESC_NULL_RECORDS = 1  # rpgpu_batch_desc.flags
+
+KAFKA_ERR_UNKNOWN_SERVER_ERROR = -1
+KAFKA_ERR_NONE = 0
+KAFKA_ERR_CORRUPT_MESSAGE = 2
+KAFKA_ERR_MESSAGE_TOO_LARGE = 10
+KAFKA_ERR_INVALID_RECORD = 87
 ARENA_TAIL_PAD = 64
 HEADER_SIZE = 61
 
@@ -162,9 +171,12 @@ def lib() -> C.CDLL:
         _sig(L.rpgpu_plan_device, _i32, _vp, _vp, _u32, _vp, _vp, _vp, _vp)
         _sig(L.rpgpu_run_device, _i32, _vp, _vp, _u32, _vp, _vp, _vp, _u64, _vp, _vp)
         _sig(L.rpgpu_crc32c_ranges_device, _i32, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp)
-        _sig(L.rpgpu_crc32c_extend, _u32, _vp, _u32, _vp, C.c_size_t)
-        _sig(L.rpgpu_internal_header_only_crc, _u32, _vp, _vp)
-        _sig(L.rpgpu_crc_record_batch, _i32, _vp, _vp, _vp, C.c_size_t)
+        _sig(L.rpgpu_crc32c_extend, _i32, _vp, _u32, _vp, C.c_size_t, C.POINTER(_u32))
+        _sig(L.rpgpu_internal_header_only_crc, _i32, _vp, _vp, C.POINTER(_u32))
+        _sig(L.rpgpu_crc_record_batch, _i32, _vp, _vp, _vp, C.c_size_t, C.POINTER(_i32))
+        _sig(L.rpgpu_eventfd, C.c_int, _vp)
+        _sig(L.rpgpu_kafka_error_code, _i32, _vp, _u32)
+        _sig(L.rpgpu_kafka_error_codes_device, _i32, _vp, _vp, _u32, _u32, _vp, _vp)
         if not hasattr(L, "rpgpu_decomp_scratch_bytes"):  # an older build (A/B timing runs)
             _LIB = L
             return _LIB
@@ -201,6 +213,7 @@ def gen() -> C.CDLL:
 EXPORTED = [
     "rpgpu_abi_version", "rpgpu_open", "rpgpu_close", "rpgpu_last_error", "rpgpu_device_info",
     "rpgpu_arena_alloc", "rpgpu_arena_free", "rpgpu_submit", "rpgpu_poll", "rpgpu_wait",
+    "rpgpu_eventfd", "rpgpu_kafka_error_code", "rpgpu_kafka_error_codes_device",
     "rpgpu_validate_scratch_bytes", "rpgpu_validate_device", "rpgpu_plan_device",
     "rpgpu_run_device", "rpgpu_crc32c_ranges_device",
     "rpgpu_crc32c_extend", "rpgpu_internal_header_only_crc", "rpgpu_crc_record_batch",

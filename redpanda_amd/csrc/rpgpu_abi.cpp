@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
+#include <sys/eventfd.h>
+#include <unistd.h>
 
 #include <mutex>
 #include <new>
@@ -59,6 +61,8 @@ hipError_t launch_uncompress_bound(uint32_t codec, const uint8_t* d_in, uint64_t
                                    hipStream_t s);
 hipError_t launch_uncompress_one(uint32_t codec, const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint64_t cap,
                                  uint64_t* d_res, hipStream_t s);
+hipError_t launch_kafka_codes(const rpgpu_batch_result* d_res, uint32_t n, uint32_t batch_max_bytes,
+                              int32_t* d_codes, hipStream_t s);
 }  // namespace rpgpu
 
 namespace {
@@ -111,8 +115,24 @@ struct rpgpu_ctx {
     std::vector<Ticket> tickets;
     uint64_t next_ticket = 1;
     bool busy = false;  // one in-flight submission per context (shard-owned)
+    int efd = -1;       // rpgpu_eventfd: signalled by a host function after each stage
     std::string err;
 };
+
+namespace {
+// runs on the HIP runtime's callback thread once the preceding work on the
+// stream completed; an eventfd write is all it does (async-signal-safe)
+void signal_efd(void* arg) {
+    const int fd = static_cast<int>(reinterpret_cast<intptr_t>(arg));
+    const uint64_t one = 1;
+    ssize_t r = write(fd, &one, sizeof(one));
+    (void)r;
+}
+hipError_t enqueue_signal(rpgpu_ctx* c) {
+    if (c->efd < 0) return hipSuccess;
+    return hipLaunchHostFunc(c->stream, signal_efd, reinterpret_cast<void*>(static_cast<intptr_t>(c->efd)));
+}
+}  // namespace
 
 namespace {
 int32_t fail(rpgpu_ctx* c, hipError_t e, const char* what) {
@@ -164,6 +184,7 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
         const int v = atoi(e);
         if (v >= 1 && v <= rpgpu::kMaxRunChunks) c->overlap.chunks = v;
     }
+    c->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     c->have_overlap = hipStreamCreateWithFlags(&c->overlap.aux, hipStreamNonBlocking) == hipSuccess;
     for (int k = 0; c->have_overlap && k <= c->overlap.chunks; k++)
         c->have_overlap = hipEventCreateWithFlags(&c->overlap.ev[k], hipEventDisableTiming) == hipSuccess;
@@ -200,7 +221,24 @@ void rpgpu_close(rpgpu_ctx* c) {
     for (int k = 0; k <= rpgpu::kMaxRunChunks; k++)
         if (c->overlap.ev[k]) (void)hipEventDestroy(c->overlap.ev[k]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->efd >= 0) close(c->efd);
     delete c;
+}
+
+int rpgpu_eventfd(rpgpu_ctx* c) { return c ? c->efd : -1; }
+
+int32_t rpgpu_kafka_error_code(const rpgpu_batch_result* r, uint32_t batch_max_bytes) {
+    if (!r) return RPGPU_KAFKA_ERR_UNKNOWN_SERVER_ERROR;
+    return rpgpu::kafka_error_code(r->verdict, r->size_bytes, batch_max_bytes);
+}
+
+int32_t rpgpu_kafka_error_codes_device(rpgpu_ctx* c, const rpgpu_batch_result* d_results, uint32_t n,
+                                       uint32_t batch_max_bytes, int32_t* d_codes, void* hip_stream) {
+    if (!c || (n && (!d_results || !d_codes))) return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_kafka_codes(d_results, n, batch_max_bytes, d_codes, s);
+    if (e != hipSuccess) return fail(c, e, "kafka codes launch");
+    return RPGPU_OK;
 }
 
 const char* rpgpu_last_error(const rpgpu_ctx* c) { return c ? c->err.c_str() : "null context"; }
@@ -391,7 +429,7 @@ int32_t rpgpu_submit(rpgpu_ctx* c, const rpgpu_batch_desc* descs, uint32_t n, co
     if ((e = hipMemcpyAsync(out_results, base + o_res, sizeof(rpgpu_batch_result) * n, hipMemcpyDeviceToHost,
                             s)) != hipSuccess ||
         (e = hipMemcpyAsync(t->h_used, base + o_used, sizeof(uint64_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
-        (e = hipEventRecord(t->ev1, s)) != hipSuccess)
+        (e = hipEventRecord(t->ev1, s)) != hipSuccess || (e = enqueue_signal(c)) != hipSuccess)
         return fail(c, e, "download");
     t->phase = 1;
     t->status = RPGPU_OK;
@@ -421,6 +459,7 @@ static int32_t advance(rpgpu_ctx* c, Ticket& t, bool block) {
                                               sizeof(rpgpu_record_index) * ncopy, hipMemcpyDeviceToHost,
                                               c->stream);
                 if (e == hipSuccess) e = hipEventRecord(t.ev2, c->stream);
+                if (e == hipSuccess) e = enqueue_signal(c);
                 if (e != hipSuccess) {
                     t.phase = 3;
                     t.status = fail(c, e, "index download");
@@ -528,24 +567,27 @@ int32_t rpgpu_uncompress(rpgpu_ctx* c, int32_t codec, const void* in, size_t n, 
     return verdict;
 }
 
-uint32_t rpgpu_crc32c_extend(rpgpu_ctx* c, uint32_t crc, const void* p, size_t n) {
-    uint32_t out = 0;
-    if (!c || (n && !p) || n > 0xffffffffu) return 0;
-    if (crc_one(c, crc, p, n, &out) != RPGPU_OK) return 0;
-    return out;
+int32_t rpgpu_crc32c_extend(rpgpu_ctx* c, uint32_t crc, const void* p, size_t n, uint32_t* out) {
+    if (!c || !out || (n && !p) || n > 0xffffffffu) return RPGPU_EINVAL;
+    return crc_one(c, crc, p, n, out);
 }
 
-uint32_t rpgpu_internal_header_only_crc(rpgpu_ctx* c, const rpgpu_rp_header* h) {
+int32_t rpgpu_internal_header_only_crc(rpgpu_ctx* c, const rpgpu_rp_header* h, uint32_t* out) {
     // model/record_utils.cc:34-55: the 57 little-endian bytes after header_crc
     // are exactly the packed image's bytes [4, 61).
-    if (!h) return 0;
-    return rpgpu_crc32c_extend(c, 0, reinterpret_cast<const uint8_t*>(h) + 4, RPGPU_HEADER_SIZE - 4);
+    if (!c || !h || !out) return RPGPU_EINVAL;
+    return rpgpu_crc32c_extend(c, 0, reinterpret_cast<const uint8_t*>(h) + 4, RPGPU_HEADER_SIZE - 4, out);
 }
 
-int32_t rpgpu_crc_record_batch(rpgpu_ctx* c, const rpgpu_rp_header* h, const void* body, size_t n) {
+int32_t rpgpu_crc_record_batch(rpgpu_ctx* c, const rpgpu_rp_header* h, const void* body, size_t n, int32_t* out) {
     // model/record_utils.cc:68-87: big-endian attrs..record_count, then body.
-    if (!h) return 0;
-    std::vector<uint8_t> buf(40 + n);
+    if (!c || !h || !out || (n && !body)) return RPGPU_EINVAL;
+    std::vector<uint8_t> buf;
+    try {
+        buf.resize(40 + n);
+    } catch (...) {
+        return RPGPU_ENOMEM;
+    }
     uint8_t* q = buf.data();
     auto be = [&](uint64_t v, int nb) {
         for (int i = 0; i < nb; i++) *q++ = (uint8_t)(v >> (8 * (nb - 1 - i)));
@@ -559,7 +601,10 @@ int32_t rpgpu_crc_record_batch(rpgpu_ctx* c, const rpgpu_rp_header* h, const voi
     be((uint32_t)h->base_sequence, 4);
     be((uint32_t)h->record_count, 4);
     if (n) memcpy(q, body, n);
-    return (int32_t)rpgpu_crc32c_extend(c, 0, buf.data(), buf.size());
+    uint32_t v = 0;
+    const int32_t st = rpgpu_crc32c_extend(c, 0, buf.data(), buf.size(), &v);
+    if (st == RPGPU_OK) *out = (int32_t)v;
+    return st;
 }
 
 }  // extern "C"

@@ -49,5 +49,28 @@ struct Overlap {
 
 void build_tables(uint32_t* out /* kTableWords */);
 
+// Produce-handler verdict -> Kafka error code (produce.cc:440-489 in its
+// order: null records, legacy error, !valid_crc, !v2_format || !batch; then
+// batch_max_bytes, produce.cc:317-324).  Shared by the host and device entry points.
+__host__ __device__ inline int32_t kafka_error_code(int32_t verdict, int32_t size_bytes, uint32_t batch_max_bytes) {
+    switch (verdict) {
+    case RPGPU_V_OK:
+        return (batch_max_bytes && (uint32_t)size_bytes > batch_max_bytes) ? RPGPU_KAFKA_ERR_MESSAGE_TOO_LARGE
+                                                                           : RPGPU_KAFKA_ERR_NONE;
+    case RPGPU_V_NULL_RECORDS:      // !part.records
+    case RPGPU_V_TOO_SMALL:         // flags uninitialised: rejected, code unpinned
+    case RPGPU_V_BAD_MAGIC:         // !v2_format (valid_crc uninitialised)
+    case RPGPU_V_REC_ATTR_EOF:      // for_each_record threw: batch unset
+    case RPGPU_V_REC_TRAILING:
+    case RPGPU_V_REC_HCOUNT_NEG:
+    case RPGPU_V_REC_UNDEFINED:
+        return RPGPU_KAFKA_ERR_INVALID_RECORD;
+    case RPGPU_V_CRC_MISMATCH:      // !valid_crc
+        return RPGPU_KAFKA_ERR_CORRUPT_MESSAGE;
+    default:                        // an exception escapes the request decoder,
+        return RPGPU_KAFKA_ERR_UNKNOWN_SERVER_ERROR;  // or not a produce-path verdict
+    }
+}
+
 }  // namespace rpgpu
 #endif

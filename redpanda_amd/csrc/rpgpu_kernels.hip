@@ -189,7 +189,8 @@ __device__ __forceinline__ void load_rows(u32x4 (&x)[kRowsPerChunk], __amdgpu_bu
 }
 
 __device__ __forceinline__ Geom desc_geometry(const rpgpu_batch_desc& d) {
-    return d.length >= (uint32_t)kHeaderSize ? geometry((int32_t)d.length) : Geom{0, 0};
+    return (d.length >= (uint32_t)kHeaderSize && !(d.flags & RPGPU_DESC_NULL_RECORDS)) ? geometry((int32_t)d.length)
+                                                                                      : Geom{0, 0};
 }
 
 // Row block at batch offset ro0 + 16*lane with bytes [0, 61) replaced by the
@@ -259,7 +260,12 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
     int64_t n;  // end of the Kafka-CRC region (trimmed batch length)
     bool body_trunc = false;
     bool fail = false;
-    if (d.format == RPGPU_FMT_KAFKA_WIRE) {
+    if (d.flags & RPGPU_DESC_NULL_RECORDS) {
+        // produce.cc:440-449: the records field was null; nothing to read
+        n = 0;
+        r.verdict = RPGPU_V_NULL_RECORDS;
+        fail = true;
+    } else if (d.format == RPGPU_FMT_KAFKA_WIRE) {
         // kafka_batch_adapter::adapt / read_header (kafka_batch_adapter.cc:32-198)
         const int32_t bl = (int32_t)H.get_be(8, 4);
         const uint64_t blen = (uint64_t)(int64_t)bl + 12u;
@@ -533,7 +539,7 @@ __global__ __launch_bounds__(256) void walk_kernel(const rpgpu_batch_desc* __res
 // ------------------------------------------------------- index-cap prepass
 // Same rule as oracle/batch.c orc_index_cap.
 __device__ __forceinline__ uint32_t index_cap(const rpgpu_batch_desc& d, const uint8_t* data) {
-    if (!(d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX))) return 0;
+    if (!(d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX)) || (d.flags & RPGPU_DESC_NULL_RECORDS)) return 0;
     const uint8_t* p = data + d.offset;
     const uint64_t len = d.length;
     if (len < (uint64_t)kHeaderSize) return 0;
@@ -687,6 +693,20 @@ __global__ __launch_bounds__(kValidateThreads) void crc_ranges_kernel(
         }
         if (l == 0) out[i] = crc;
     }
+}
+
+// produce-handler error codes (rpgpu_kafka_error_codes_device)
+__global__ __launch_bounds__(256) void kafka_codes_kernel(const rpgpu_batch_result* __restrict__ res, uint32_t n,
+                                                          uint32_t batch_max_bytes, int32_t* __restrict__ codes) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) codes[i] = kafka_error_code(res[i].verdict, res[i].size_bytes, batch_max_bytes);
+}
+
+hipError_t launch_kafka_codes(const rpgpu_batch_result* d_res, uint32_t n, uint32_t batch_max_bytes,
+                              int32_t* d_codes, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    kafka_codes_kernel<<<(n + 255) / 256, 256, 0, s>>>(d_res, n, batch_max_bytes, d_codes);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------ launchers

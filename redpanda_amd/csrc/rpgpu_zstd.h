@@ -19,9 +19,13 @@
 //     last block skips the content-size check, the block output is bounded by
 //     the ring buffer left, which wraps when it is smaller than the frame);
 //   * the workspace rule: a frame whose in+out ring buffers exceed what
-//     ZSTD_estimateDStreamSize(8 MiB) leaves is ZSTD_error_memory_allocation
-//     -> std::bad_alloc (RPGPU_V_DECOMP_BAD_ALLOC); windows above 128 MiB+1 are
-//     errors; buffers are reused across the frames of one call;
+//     ZSTD_estimateDStreamSize(8 MiB) leaves is ZSTD_error_memory_allocation;
+//     windows above 128 MiB+1 are frameParameter_windowTooLarge; buffers are
+//     reused across the frames of one call.  Both are plain errors
+//     (RPGPU_V_DECOMP_ERROR): throw_zstd_err (stream_zstd.cc:29-36) compares
+//     the raw size_t return with the enum ZSTD_error_memory_allocation (64),
+//     which never matches, so its std::bad_alloc branch is dead and every
+//     zstd error is a std::runtime_error;
 //   * inside a block: the literals section (raw, RLE, Huffman 1 or 4 streams,
 //     repeat), HUF_readStats with FSE-coded weights, HUF_selectDecoder's X1/X2
 //     choice (the two differ only in how the last symbol of a stream is
@@ -67,7 +71,7 @@ using rpcodec::le16;
 using rpcodec::le32;
 using rpcodec::le64;
 
-constexpr int32_t V_OK = 0, V_ERROR = 30, V_BAD_ALLOC = 31, V_OVERFLOW = 34;
+constexpr int32_t V_OK = 0, V_ERROR = 30, V_OVERFLOW = 34;
 constexpr uint32_t kMagic = 0xFD2FB528u, kSkipMagic = 0x184D2A50u, kSkipMask = 0xFFFFFFF0u;
 constexpr uint64_t kBlockMax = 128u * 1024u;          // ZSTD_BLOCKSIZE_MAX
 constexpr uint64_t kStage = 64u * 1024u;              // stream_zstd d_buffer
@@ -1210,7 +1214,7 @@ RPC_HD int32_t uncompress_impl(const uint8_t* in, uint64_t n, uint8_t* out, uint
             const uint64_t need_in = h.bsm < 4 ? 4 : h.bsm;
             const uint64_t ring = W + (W < kBlockMax ? W : kBlockMax) + 64;
             const uint64_t need_out = h.fcs < ring ? h.fcs : ring;
-            if (!adapt(bufs, need_in, need_out)) return V_BAD_ALLOC;
+            if (!adapt(bufs, need_in, need_out)) return RPZ_FAIL(V_ERROR);  // memory_allocation: runtime_error
         }
         uint64_t decoded = 0, ostart = 0;
         bool done = false;

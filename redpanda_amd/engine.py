@@ -273,18 +273,61 @@ class Engine:
     def crc32c_extend(self, crc: int, data: bytes | np.ndarray) -> int:
         buf = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
-        return int(self._lib.rpgpu_crc32c_extend(self._ctx, crc & 0xFFFFFFFF,
-                                                 buf.ctypes.data if buf.size else None, buf.size))
+        out = C.c_uint32()
+        rc = self._lib.rpgpu_crc32c_extend(self._ctx, crc & 0xFFFFFFFF, buf.ctypes.data if buf.size else None,
+                                           buf.size, C.byref(out))
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_crc32c_extend: {rc} {self.last_error()}")
+        return int(out.value)
 
     def internal_header_only_crc(self, hdr: np.ndarray) -> int:
         h = np.ascontiguousarray(hdr, dtype=abi.RP_HEADER_DTYPE).reshape(1)
-        return int(self._lib.rpgpu_internal_header_only_crc(self._ctx, h.ctypes.data))
+        out = C.c_uint32()
+        rc = self._lib.rpgpu_internal_header_only_crc(self._ctx, h.ctypes.data, C.byref(out))
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_internal_header_only_crc: {rc} {self.last_error()}")
+        return int(out.value)
 
     def crc_record_batch(self, hdr: np.ndarray, body: bytes | np.ndarray) -> int:
         h = np.ascontiguousarray(hdr, dtype=abi.RP_HEADER_DTYPE).reshape(1)
         b = np.ascontiguousarray(np.frombuffer(bytes(body), dtype=np.uint8))
-        return int(self._lib.rpgpu_crc_record_batch(self._ctx, h.ctypes.data,
-                                                    b.ctypes.data if b.size else None, b.size))
+        out = C.c_int32()
+        rc = self._lib.rpgpu_crc_record_batch(self._ctx, h.ctypes.data, b.ctypes.data if b.size else None,
+                                              b.size, C.byref(out))
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_crc_record_batch: {rc} {self.last_error()}")
+        return int(out.value)
+
+    # -- produce-handler glue -----------------------------------------------------------
+    def eventfd(self) -> int:
+        return int(self._lib.rpgpu_eventfd(self._ctx))
+
+    def submit_async(self, data: np.ndarray, descs: np.ndarray, index_cap: int | None = None):
+        """rpgpu_submit without waiting: returns (ticket, results, index, used, keep)
+        -- `keep` holds the host buffers alive until the ticket completes."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        descs = np.ascontiguousarray(descs, dtype=abi.DESC_DTYPE)
+        n = len(descs)
+        if index_cap is None:
+            index_cap = int(descs["length"].astype(np.uint64).sum() // 2) + 1
+        results = np.zeros(n, dtype=abi.RESULT_DTYPE)
+        index = np.zeros(max(index_cap, 1), dtype=abi.INDEX_DTYPE)
+        used = C.c_uint64()
+        ticket = C.c_uint64()
+        rc = self._lib.rpgpu_submit(self._ctx, descs.ctypes.data, n, data.ctypes.data, data.nbytes,
+                                    results.ctypes.data, index.ctypes.data, index_cap,
+                                    C.byref(used), C.byref(ticket))
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_submit: {rc} {self.last_error()}")
+        return ticket.value, results, index, used, (data, descs)
+
+    def poll(self, ticket: int) -> int:
+        return int(self._lib.rpgpu_poll(self._ctx, ticket))
+
+    @staticmethod
+    def kafka_error_code(result: np.ndarray, batch_max_bytes: int = 0) -> int:
+        r = np.ascontiguousarray(result, dtype=abi.RESULT_DTYPE).reshape(1)
+        return int(abi.lib().rpgpu_kafka_error_code(r.ctypes.data, batch_max_bytes))
 
 
 # ---- workload construction (librpgen.so) -----------------------------------------

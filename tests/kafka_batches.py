@@ -70,3 +70,39 @@ def arena(batches: list[bytes], fmt: int = WIRE, ops: int = 15,
     descs["format"] = fmt
     descs["ops"] = ops
     return data, descs
+
+
+def zstd_reheader(frame: bytes, wlog: int | None, fcs="keep", mantissa: int = 0) -> bytes:
+    """Re-writes a zstd frame's header (RFC 8878 §3.1.1.1) over the same blocks:
+    `wlog` = window descriptor exponent (None: single-segment, window = content
+    size), `fcs` = content size field ("keep", None = absent, or a value).
+    Blocks are untouched, so the frame stays valid while the window covers
+    its offsets; used to reach the decoder's workspace / window limits
+    (stream_zstd.cc:29-87) with frames the reference's compressor never makes."""
+    fhd = frame[4]
+    did, ss, fid, csum = fhd & 3, (fhd >> 5) & 1, fhd >> 6, (fhd >> 2) & 1
+    pos = 5 + (0 if ss else 1)
+    dsz = (0, 1, 2, 4)[did]
+    pos += dsz
+    fsz = (ss, 2, 4, 8)[fid]
+    old = None
+    if fsz:
+        raw = int.from_bytes(frame[pos:pos + fsz], "little")
+        old = raw + 256 if fsz == 2 else raw
+    blocks = frame[pos + fsz:]
+    size = old if fcs == "keep" else fcs
+    if wlog is None and size is None:
+        raise ValueError("a single-segment frame needs a content size")
+    if size is None:
+        fflag, field = 0, b""
+    elif wlog is None and size < 256:
+        fflag, field = 0, bytes([size])
+    elif 256 <= size < 65536 + 256:
+        fflag, field = 1, (size - 256).to_bytes(2, "little")
+    elif size < 1 << 32:
+        fflag, field = 2, size.to_bytes(4, "little")
+    else:
+        fflag, field = 3, size.to_bytes(8, "little")
+    new_fhd = (fflag << 6) | ((1 if wlog is None else 0) << 5) | (csum << 2)
+    wd = b"" if wlog is None else bytes([((wlog - 10) << 3) | mantissa])
+    return frame[:4] + bytes([new_fhd]) + wd + field + blocks

@@ -180,7 +180,7 @@ Bytes lib_frame(const Bytes& src) {
     ZSTD_CCtx* c = ZSTD_createCCtx();
     const int levels[] = {-5, -1, 1, 2, 3, 3, 3, 5, 9, 19};
     ck(ZSTD_CCtx_setParameter(c, ZSTD_c_compressionLevel, levels[below(10)]));
-    if (below(3) == 0) ck(ZSTD_CCtx_setParameter(c, ZSTD_c_windowLog, 10 + (int)below(12)));
+    if (below(3) == 0) ck(ZSTD_CCtx_setParameter(c, ZSTD_c_windowLog, 10 + (int)below(below(8) ? 12 : 15)));
     ck(ZSTD_CCtx_setParameter(c, ZSTD_c_checksumFlag, below(4) == 0));
     const bool content = below(4) != 0;
     ck(ZSTD_CCtx_setParameter(c, ZSTD_c_contentSizeFlag, content));
@@ -215,6 +215,18 @@ Bytes lib_frame(const Bytes& src) {
         ck(r);
         out.resize(r);
     }
+    ZSTD_freeCCtx(c);
+    return out;
+}
+
+// the reference's compressor settings (stream_zstd.cc:89-151): level 3, pledged size
+Bytes lib_frame_plain(const Bytes& src) {
+    Bytes out(ZSTD_compressBound(src.size()) + 64);
+    ZSTD_CCtx* c = ZSTD_createCCtx();
+    ck(ZSTD_CCtx_setPledgedSrcSize(c, src.size()));
+    const size_t r = ZSTD_compress2(c, out.data(), out.size(), src.data(), src.size());
+    ck(r);
+    out.resize(r);
     ZSTD_freeCCtx(c);
     return out;
 }
@@ -300,6 +312,56 @@ void compare(const Bytes& in) {
     }
 }
 
+// Window / workspace limits (stream_zstd.cc:29-87): the frame's own blocks
+// under a rewritten header -- every window exponent 10..31 with mantissas 0
+// and 7, content size absent / kept / single-segment -- around the 8 MiB
+// workspace (ring = window + 128 KiB + 64 unless the content size is
+// smaller) and ZSTD_MAXWINDOWSIZE_DEFAULT.
+Bytes reheader(const Bytes& f, int wlog, int mant, int fcs_mode /* 0 none, 1 keep, 2 single */) {
+    const uint8_t fhd = f[4];
+    const unsigned did = fhd & 3, ss = (fhd >> 5) & 1, fid = fhd >> 6, csum = (fhd >> 2) & 1;
+    size_t pos = 5 + (ss ? 0 : 1) + (const unsigned[]){0, 1, 2, 4}[did];
+    const size_t fsz = (const size_t[]){ss, 2, 4, 8}[fid];
+    uint64_t fcs = 0;
+    for (size_t k = 0; k < fsz; k++) fcs |= (uint64_t)f[pos + k] << (8 * k);
+    if (fsz == 2) fcs += 256;
+    Bytes o(f.begin(), f.begin() + 4);
+    const bool single = fcs_mode == 2;
+    unsigned fflag = 0;
+    Bytes field;
+    if (fcs_mode) {
+        if (single && fcs < 256) {
+            field.push_back((uint8_t)fcs);
+        } else if (fcs >= 256 && fcs < 65536 + 256) {
+            fflag = 1;
+            field.push_back((uint8_t)(fcs - 256));
+            field.push_back((uint8_t)((fcs - 256) >> 8));
+        } else {
+            fflag = 2;
+            for (int k = 0; k < 4; k++) field.push_back((uint8_t)(fcs >> (8 * k)));
+        }
+    }
+    o.push_back((uint8_t)((fflag << 6) | ((single ? 1u : 0u) << 5) | (csum << 2)));
+    if (!single) o.push_back((uint8_t)(((wlog - 10) << 3) | mant));
+    o.insert(o.end(), field.begin(), field.end());
+    o.insert(o.end(), f.begin() + pos + fsz, f.end());
+    return o;
+}
+
+void check_windows() {
+    for (size_t n : {(size_t)(60 << 10), (size_t)(64 << 10), (size_t)(100 << 10), (size_t)(300 << 10)}) {
+        Bytes src(n);
+        for (size_t i = 0; i < n; i++) src[i] = (uint8_t)("kafka redpanda offset log "[(i * 7 + i / 13) % 26]);
+        const Bytes f = lib_frame_plain(src);
+        for (int mode = 0; mode < 3; mode++)
+            for (int wl = 10; wl <= 31; wl++)
+                for (int mant : {0, 7}) {
+                    if (mode == 2 && (wl > 10 || mant)) continue;
+                    compare(reheader(f, wl, mant, mode));
+                }
+    }
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -324,6 +386,7 @@ int main(int argc, char** argv) {
         return 0;
     }
     check_select();
+    check_windows();
     check_ncount(cases * 4);
     for (long i = 0; i < cases; i++) {
         Bytes b = body();

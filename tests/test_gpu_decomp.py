@@ -160,3 +160,29 @@ def test_uncompress_scalar_mirror(eng):
         assert gv == ov, (codec, len(c), gv, ov)
         if ov == 0:
             assert gout == oout, (codec, len(c))
+
+
+def test_zstd_window_limits(eng):
+    """Frames past the 8 MiB static workspace (windowLog 24, content size
+    unknown: ZSTD_error_memory_allocation) and past ZSTD_MAXWINDOWSIZE_DEFAULT
+    (windowLog 28: frameParameter_windowTooLarge) are DECOMP_ERROR like every
+    zstd error (stream_zstd.cc:29-36: the bad_alloc branch never matches);
+    with a content size the staging buffer holds, the single-pass decode
+    takes them.  Scalar mirror and arena path, against the oracle."""
+    from redpanda_amd import abi
+    from test_zstd_window import window_cases
+
+    cases = list(window_cases())
+    for name, frame, want in cases:
+        gv, gout = eng.uncompress(4, frame, cap=1 << 20)
+        ov, oout = orc.uncompress(4, frame, cap=1 << 20)
+        assert ov == want and gv == ov, (name, gv, ov)
+        if ov == abi.V_OK:
+            assert gout == oout, name
+    wanted = {n: w for n, _, w in cases}
+    assert wanted["wlog24_nofcs"] == abi.V_DECOMP_ERROR and wanted["wlog28_fcs100k"] == abi.V_DECOMP_ERROR
+    # the same frames as record bodies of an arena (payload bytes only: the
+    # walk of a decoded OK batch then reports its record verdict)
+    bs = [batch(frame, fmt=WIRE, record_count=0, attrs=4) for _, frame, _ in cases]
+    data, descs = arena(bs, fmt=WIRE, ops=OPS)
+    compare(eng.decompress_arena(data, descs), data, descs)
