@@ -92,7 +92,8 @@ enum rpgpu_verdict {
      * zstd error. */
     RPGPU_V_LZ4_TRAILING = 32,     /* unconsumed input after LZ4 frame end        */
     RPGPU_V_DECOMP_UNSUPPORTED = 33,/* codec not implemented on this engine (gzip) */
-    RPGPU_V_DECOMP_OVERFLOW = 34,  /* decompressed size exceeds the output slot   */
+    RPGPU_V_DECOMP_OVERFLOW = 34,  /* decompressed size exceeds the output slot, or
+                                      its bound exceeds opts.max_decoded_batch */
     /* multi-batch record sets (kafka/protocol/batch_reader.cc:50-58) */
     RPGPU_V_SET_HEADER_SHORT = 36, /* < 61 bytes left for the next batch header:
                                       corrupt_message "Invalid kafka header parsing" */
@@ -179,7 +180,15 @@ typedef struct rpgpu_opts {
     uint32_t flags;        /* reserved, 0 */
     uint32_t max_batches;  /* per-submission capacity hint (0 = default)   */
     uint64_t max_arena;    /* per-submission arena bytes hint (0 = default) */
+    /* decompression: ceiling on one batch's output slot (61-byte header +
+     * the decoded-size bound read off its frame + slack).  A batch above it
+     * gets RPGPU_V_DECOMP_OVERFLOW and no slot, so one hostile frame (e.g. a
+     * 1 MiB body of RLE blocks bounding 32 GB) cannot inflate the shared
+     * output plan.  0 = RPGPU_DEFAULT_MAX_DECODED_BATCH.  Not a reference
+     * limit: there the outcome depends on the broker's free memory. */
+    uint64_t max_decoded_batch;
 } rpgpu_opts;
+#define RPGPU_DEFAULT_MAX_DECODED_BATCH (64ull << 20)
 
 typedef struct rpgpu_ctx rpgpu_ctx;
 typedef uint64_t rpgpu_ticket;

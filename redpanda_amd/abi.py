@@ -120,6 +120,13 @@ class GenSpec(C.Structure):
                 ("corrupt_mask", C.c_uint32), ("base_timestamp", C.c_int64)]
 
 
+class Opts(C.Structure):  # rpgpu_opts
+    _fields_ = [("flags", C.c_uint32), ("max_batches", C.c_uint32), ("max_arena", C.c_uint64),
+                ("max_decoded_batch", C.c_uint64)]
+
+
+DEFAULT_MAX_DECODED_BATCH = 64 << 20
+
 _vp = C.c_void_p
 _u32 = C.c_uint32
 _u64 = C.c_uint64

@@ -50,7 +50,7 @@ hipError_t launch_sets_run(const rpgpu_batch_desc* d_sets, uint32_t n, const uin
                            int grid, hipStream_t s, const Overlap* ov);
 hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                               const rpgpu_batch_result* d_vres, uint64_t* d_out_bytes, void* d_scratch,
-                              hipStream_t s);
+                              uint64_t max_decoded, hipStream_t s);
 hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                              const rpgpu_batch_result* d_vres, rpgpu_decomp_result* d_dres, uint8_t* d_out,
                              uint64_t out_cap, rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_vres2,
@@ -115,6 +115,7 @@ struct rpgpu_ctx {
     std::vector<Ticket> tickets;
     uint64_t next_ticket = 1;
     bool busy = false;  // one in-flight submission per context (shard-owned)
+    uint64_t max_decoded = RPGPU_DEFAULT_MAX_DECODED_BATCH;  // opts.max_decoded_batch
     int efd = -1;       // rpgpu_eventfd: signalled by a host function after each stage
     std::string err;
 };
@@ -149,9 +150,9 @@ extern "C" {
 int32_t rpgpu_abi_version(void) { return RPGPU_ABI_VERSION; }
 
 rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
-    (void)opts;
     rpgpu_ctx* c = new (std::nothrow) rpgpu_ctx();
     if (!c) return nullptr;
+    if (opts && opts->max_decoded_batch) c->max_decoded = opts->max_decoded_batch;
     c->device = device;
     if (hipSetDevice(device) != hipSuccess) {
         delete c;
@@ -306,7 +307,8 @@ int32_t rpgpu_decomp_plan_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, 
                                  uint64_t* d_out_bytes, void* d_scratch, void* hip_stream) {
     if (!c || (n && (!d_descs || !d_data || !d_results || !d_scratch))) return RPGPU_EINVAL;
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
-    hipError_t e = rpgpu::launch_decomp_plan(d_descs, n, d_data, d_results, d_out_bytes, d_scratch, s);
+    hipError_t e = rpgpu::launch_decomp_plan(d_descs, n, d_data, d_results, d_out_bytes, d_scratch,
+                                              c->max_decoded, s);
     if (e != hipSuccess) return fail(c, e, "decomp plan launch");
     return RPGPU_OK;
 }
@@ -549,6 +551,10 @@ int32_t rpgpu_uncompress(rpgpu_ctx* c, int32_t codec, const void* in, size_t n, 
         (e = hipStreamSynchronize(c->stream)) != hipSuccess)
         return fail(c, e, "download");
     const uint64_t bound = h[0];
+    if (bound + RPGPU_HEADER_SIZE + 128 > c->max_decoded) {  // the arena path's per-batch ceiling
+        *out_len = bound;
+        return RPGPU_V_DECOMP_OVERFLOW;
+    }
     if ((e = c->small_out.reserve(bound + 256)) != hipSuccess) return fail(c, e, "device buffer");
     uint8_t* dout = static_cast<uint8_t*>(c->small_out.p);
     if ((e = rpgpu::launch_uncompress_one((uint32_t)codec, base, n, dout, bound, meta, c->stream)) != hipSuccess)

@@ -74,6 +74,10 @@ Parts parts(void* p, uint32_t n) {
 
 size_t decomp_scratch_bytes(uint32_t n) { return zws_offset(n) + (size_t)zstd_lanes(n) * sizeof(rpzstd::Ws); }
 
+// slot[i] of a batch whose bound exceeds the per-batch ceiling: no output
+// reserved (the scan counts 0), verdict DECOMP_OVERFLOW
+constexpr uint64_t kOverCeiling = 1ull << 63;
+
 __device__ __forceinline__ bool decomp_wanted(const rpgpu_batch_desc& d, const rpgpu_batch_result& v) {
     return (d.ops & RPGPU_OP_DECOMP) && v.verdict == RPGPU_V_OK && v.codec != 0;
 }
@@ -82,10 +86,11 @@ __device__ __forceinline__ bool decomp_wanted(const rpgpu_batch_desc& d, const r
 __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
     const rpgpu_batch_result* __restrict__ vres, uint64_t* __restrict__ slot, uint64_t* __restrict__ local,
-    uint64_t* __restrict__ block_sum) {
+    uint64_t* __restrict__ block_sum, uint64_t max_decoded) {
     __shared__ uint64_t wsum[kScanBlock / 64];
     const uint32_t i = blockIdx.x * kScanBlock + threadIdx.x;
     uint64_t sz = 0;
+    bool over = false;
     if (i < n) {
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
@@ -95,6 +100,10 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
             const uint8_t* b = data + d.offset + kHeaderSize;
             const uint64_t bound = v.codec == 4 ? rpzstd::bound(b, body) : rpcodec::uncompress_bound(v.codec, b, body);
             sz = (kHeaderSize + bound + rpcodec::kSlack + 15) & ~(uint64_t)15;
+            if (bound > max_decoded || sz > max_decoded) {
+                sz = 0;
+                over = true;
+            }
         }
     }
     const uint32_t l = lane_id();
@@ -110,7 +119,7 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
     uint64_t wbase = 0;
     for (uint32_t k = 0; k < wv; k++) wbase += wsum[k];
     if (i < n) {
-        slot[i] = sz;
+        slot[i] = over ? kOverCeiling : sz;
         local[i] = wbase + x - sz;
     }
     if (threadIdx.x == kScanBlock - 1) {
@@ -190,11 +199,14 @@ __global__ __launch_bounds__(256) void decomp_kernel(
     const bool want = decomp_wanted(d, v);
     if (want && v.codec == 4) return;  // zstd_kernel
     const uint64_t off = block_base[i / kScanBlock] + local[i];
-    const uint64_t sz = slot[i];
+    uint64_t sz = slot[i];
     int32_t verdict = RPGPU_V_SKIPPED;
     uint64_t len = 0;
     if (want) {
-        if (sz == 0) {
+        if (sz == kOverCeiling) {
+            sz = 0;
+            verdict = RPGPU_V_DECOMP_OVERFLOW;
+        } else if (sz == 0) {
             verdict = RPGPU_V_DECOMP_UNSUPPORTED;  // gzip
         } else if (off + sz > out_cap) {
             verdict = RPGPU_V_DECOMP_OVERFLOW;  // caller's buffer smaller than the plan
@@ -223,6 +235,7 @@ __global__ __launch_bounds__(256, RPZ_MIN_WAVES) void zstd_kernel(
     rpgpu_batch_desc* __restrict__ out_descs, rpzstd::Ws* __restrict__ wsbuf) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lanes = gridDim.x * blockDim.x;
+    if (g >= n) return;  // lanes past the arena own no workspace
     rpzstd::Ws& ws = wsbuf[g];
 #if RPZ_PROF
     const uint64_t k0 = RPZ_CLK();
@@ -234,10 +247,13 @@ __global__ __launch_bounds__(256, RPZ_MIN_WAVES) void zstd_kernel(
         const rpgpu_batch_result v = vres[i];
         if (!decomp_wanted(d, v) || v.codec != 4) continue;
         const uint64_t off = block_base[i / kScanBlock] + local[i];
-        const uint64_t sz = slot[i];
+        uint64_t sz = slot[i];
         int32_t verdict;
         uint64_t len = 0;
-        if (off + sz > out_cap) {
+        if (sz == kOverCeiling) {
+            sz = 0;
+            verdict = RPGPU_V_DECOMP_OVERFLOW;
+        } else if (off + sz > out_cap) {
             verdict = RPGPU_V_DECOMP_OVERFLOW;
         } else {
             verdict = rpzstd::uncompress(data + d.offset + kHeaderSize, (uint64_t)(uint32_t)v.size_bytes - kHeaderSize,
@@ -249,7 +265,7 @@ __global__ __launch_bounds__(256, RPZ_MIN_WAVES) void zstd_kernel(
 #endif
     }
 #if RPZ_PROF
-    if (g < 4 || g == lanes - 1)  // diagnostics build: phase clocks of a few lanes
+    if (g < 4 || g == (n < lanes ? n : lanes) - 1)  // diagnostics build: phase clocks of a few lanes
         printf("RPZ_PROF lane=%u batches=%u total=%llu lit=%llu seq=%llu n_lit=%llu n_seq=%llu\n", g, nb_done,
                (unsigned long long)(RPZ_CLK() - k0), (unsigned long long)ws.t_lit, (unsigned long long)ws.t_seq,
                (unsigned long long)ws.n_lit, (unsigned long long)ws.n_seq);
@@ -286,11 +302,12 @@ __global__ void uncompress_one_kernel(uint32_t codec, const uint8_t* in, uint64_
 // ------------------------------------------------------------ launchers
 hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                               const rpgpu_batch_result* d_vres, uint64_t* d_out_bytes, void* d_scratch,
-                              hipStream_t s) {
+                              uint64_t max_decoded, hipStream_t s) {
     if (n == 0) return d_out_bytes ? hipMemsetAsync(d_out_bytes, 0, sizeof(uint64_t), s) : hipSuccess;
     const Parts p = parts(d_scratch, n);
     const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
-    decomp_caps_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum);
+    decomp_caps_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
+                                                 max_decoded);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_block_scan(p.block_sum, nb, d_out_bytes, s);

@@ -341,8 +341,8 @@ RPC_HD uint64_t bits_at(Bits& b, int64_t lo, uint32_t n) {
     uint64_t v;
     if (off < 64)
         v = off ? (b.win >> off) | (b.win_hi << (64 - off)) : b.win;
-    else
-        v = b.win_hi >> (off - 64);
+    else  // off == 128 only for n == 0 (a 0-bit read at the window top)
+        v = off < 128 ? b.win_hi >> (off - 64) : 0;
     return v & lomask(n);
 }
 RPC_HD uint64_t read_bits(Bits& b, uint32_t n) {  // BIT_readBits (lookBits + skip)

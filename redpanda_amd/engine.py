@@ -19,9 +19,10 @@ class EngineError(RuntimeError):
 class Engine:
     """One rpgpu context (one per Seastar shard x GPU in the reference's terms)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, max_decoded_batch: int = 0):
         self._lib = abi.lib()
-        self._ctx = self._lib.rpgpu_open(device, None)
+        opts = abi.Opts(0, 0, 0, max_decoded_batch)
+        self._ctx = self._lib.rpgpu_open(device, C.byref(opts))
         if not self._ctx:
             raise EngineError(f"rpgpu_open({device}) failed (no usable HIP device?)")
         self.device = device

@@ -20,6 +20,7 @@
 #include <random>
 #include <vector>
 
+#include "rpgpu.h"
 #include "rpgpu_codec.h"
 
 extern "C" {
@@ -324,12 +325,17 @@ Bytes snappy_hand() {
 }
 
 // ---- compare
+bool g_exact = false;
 void check(int codec, const Bytes& in, const char* what, long id) {
     const uint64_t n = in.size();
-    Bytes ib(n + 128, 0xA5);  // bytes past the input: garbage, as in an arena
+    // bytes past the input: garbage, as in an arena.  --exact: exactly the
+    // device geometry (RPGPU_ARENA_TAIL_PAD readable bytes past the input, an
+    // output slot of bound + kSlack) so a sanitizer build flags any access
+    // beyond what the GPU slot allows
+    Bytes ib(n + (g_exact ? RPGPU_ARENA_TAIL_PAD : 128), 0xA5);
     if (n) memcpy(ib.data(), in.data(), n);
     const uint64_t bound = rpcodec::uncompress_bound((uint32_t)codec, ib.data(), n);
-    Bytes ob(bound + rpcodec::kSlack + 64, 0x5A);
+    Bytes ob(bound + rpcodec::kSlack + (g_exact ? 0 : 64), 0x5A);
     uint64_t glen = 0;
     const int32_t gv = rpcodec::uncompress((uint32_t)codec, ib.data(), n, ob.data(), bound, &glen);
     const size_t ocap = bound + (1u << 20);
@@ -371,6 +377,7 @@ int main(int argc, char** argv) {
     for (int a = 1; a + 1 < argc; a += 2) {
         if (!strcmp(argv[a], "--cases")) cases = atol(argv[a + 1]);
         if (!strcmp(argv[a], "--seed")) seed = strtoull(argv[a + 1], nullptr, 0);
+        if (!strcmp(argv[a], "--exact")) g_exact = atoi(argv[a + 1]) != 0;
     }
     rng.seed(seed);
     for (long c = 0; c < cases; c++) {

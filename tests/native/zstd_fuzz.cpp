@@ -22,6 +22,7 @@
 #include <random>
 #include <vector>
 
+#include "rpgpu.h"
 #include "rpgpu_zstd.h"
 
 extern "C" {
@@ -273,14 +274,16 @@ void mutate(Bytes& f) {
     }
 }
 
+bool g_exact = false;
 void compare(const Bytes& in) {
     n_cases++;
     Bytes padded = in;
-    padded.resize(in.size() + 64);
+    padded.resize(in.size() + RPGPU_ARENA_TAIL_PAD);  // the arena's readable tail
     for (size_t k = in.size(); k < padded.size(); k++) padded[k] = (uint8_t)rng();
     const uint8_t* ip = padded.data();
     const uint64_t cap = rpzstd::bound(ip, in.size());
-    Bytes eout(cap + 1);
+    // --exact: the device slot geometry (bound + kSlack) for sanitizer builds
+    Bytes eout(g_exact ? cap + rpcodec::kSlack : cap + 1);
     static rpzstd::Ws ws;
     uint64_t elen = 0;
     const int32_t ev = rpzstd::uncompress(ip, in.size(), eout.data(), cap, &elen, ws);
@@ -372,6 +375,7 @@ int main(int argc, char** argv) {
         if (!strcmp(argv[a], "--cases")) cases = atol(argv[a + 1]);
         if (!strcmp(argv[a], "--seed")) seed = strtoull(argv[a + 1], nullptr, 0);
         if (!strcmp(argv[a], "--replay")) replay = argv[a + 1];
+        if (!strcmp(argv[a], "--exact")) g_exact = atoi(argv[a + 1]) != 0;
     }
     rng.seed(seed);
     if (replay) {

@@ -186,3 +186,55 @@ def test_zstd_window_limits(eng):
     bs = [batch(frame, fmt=WIRE, record_count=0, attrs=4) for _, frame, _ in cases]
     data, descs = arena(bs, fmt=WIRE, ops=OPS)
     compare(eng.decompress_arena(data, descs), data, descs)
+
+
+def rle_frame(blocks: int, content_size: bool) -> bytes:
+    """A zstd frame of `blocks` RLE blocks of 128 KiB each (4 bytes apiece on
+    the wire): the worst output-per-input-byte a frame can claim."""
+    import struct
+
+    bh = struct.pack("<I", (1 << 1) | ((128 << 10) << 3))[:3]  # RLE block, 131072 bytes
+    last = struct.pack("<I", 1 | (1 << 1) | ((128 << 10) << 3))[:3]
+    body = b"".join(bh + b"x" for _ in range(blocks - 1)) + last + b"y"
+    if content_size:
+        return b"\x28\xb5\x2f\xfd" + bytes([0x80, (17 - 10) << 3]) + struct.pack("<I", blocks << 17) + body
+    return b"\x28\xb5\x2f\xfd" + bytes([0x00, (17 - 10) << 3]) + body
+
+
+def test_decoded_size_ceiling(built):
+    """a batch whose decoded-size bound exceeds the per-batch
+    ceiling (opts.max_decoded_batch) gets DECOMP_OVERFLOW and no output slot;
+    every other batch of the arena -- before and after it -- decodes as the
+    oracle does, and the plan does not grow by the hostile batch's bound."""
+    from redpanda_amd import abi, engine
+
+    with engine.Engine(0, max_decoded_batch=4 << 20) as e:
+        rng = np.random.default_rng(17)
+        good = [(orc.compress(c, b"".join(records(rng, 20, 4, 300, text=True))), c) for c in (3, 4, 2, 4)]
+        hostile = rle_frame(64, content_size=False)  # 8 MiB of output from 266 bytes
+        bodies = good[:2] + [(hostile, 4)] + good[2:]
+        bs = [batch(c, fmt=WIRE, record_count=20, attrs=codec) for c, codec in bodies]
+        data, descs = arena(bs, fmt=WIRE, ops=OPS)
+        got = e.decompress_arena(data, descs)
+        v = got["dres"]["verdict"]
+        assert v[2] == abi.V_DECOMP_OVERFLOW and got["dres"]["out_cap"][2] == 0
+        assert got["out_bytes"] < 2 << 20
+        keep = np.array([0, 1, 3, 4])
+        data2, descs2 = arena([bs[i] for i in keep], fmt=WIRE, ops=OPS)
+        want = compare(e.decompress_arena(data2, descs2), data2, descs2)
+        assert np.array_equal(v[keep], want["verdicts"])
+        assert np.array_equal(got["dres"]["out_len"][keep], want["out_len"])
+        # the scalar mirror applies the same ceiling
+        gv, _ = e.uncompress(4, hostile, cap=16 << 20)
+        assert gv == abi.V_DECOMP_OVERFLOW
+    # under the default ceiling the same frame decodes, as the oracle does
+    gv, gout = eng_default_uncompress(hostile)
+    ov, oout = orc.uncompress(4, hostile, cap=16 << 20)
+    assert gv == ov == abi.V_OK and gout == oout
+
+
+def eng_default_uncompress(frame):
+    from redpanda_amd import engine
+
+    with engine.Engine(0) as e:
+        return e.uncompress(4, frame, cap=16 << 20)
