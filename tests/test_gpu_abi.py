@@ -108,7 +108,7 @@ def test_poll_and_eventfd(eng):
 def test_null_records_and_kafka_codes(eng):
     import torch
 
-    spec = engine.make_spec(seed=0x5EED00AC, partitions=4, records_per_batch=5, key_len=3, value_len=90,
+    spec = engine.make_spec(seed=0x5EED00AC, partitions=4, records_per_batch=1, body_min=7, body_max=3000,
                             corrupt_ppm=300_000, corrupt_mask=0x1FF)
     data, descs = engine.build_arena(spec, 600)
     descs["flags"][::7] = abi.DESC_NULL_RECORDS
