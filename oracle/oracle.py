@@ -168,7 +168,8 @@ def compress(codec: int, data) -> bytes:
 
 
 def decompress_arena(data: np.ndarray, descs: np.ndarray, results: np.ndarray, caps,
-                     codecs=(2, 3), nthreads: int = 1, out: np.ndarray | None = None) -> dict:
+                     codecs=(2, 3), nthreads: int = 1, out: np.ndarray | None = None,
+                     fast_crc: bool = False) -> dict:
     """Reference outcome of the decompress path for an arena already validated
     (`results` = validate_arena's or the engine's validation results, which
     agree): storage::internal::maybe_decompress_batch_sync
@@ -195,7 +196,7 @@ def decompress_arena(data: np.ndarray, descs: np.ndarray, results: np.ndarray, c
     lib().orc_decompress_batches(descs.ctypes.data, n, data.ctypes.data, results.ctypes.data, mask,
                                  out.ctypes.data, offs.ctypes.data, caps.ctypes.data,
                                  verdicts.ctypes.data, lens.ctypes.data, rdescs.ctypes.data, nthreads)
-    rres, ridx, rused = validate_arena(out, rdescs, nthreads=nthreads)
+    rres, ridx, rused = validate_arena(out, rdescs, nthreads=nthreads, fast_crc=fast_crc)
     return dict(verdicts=verdicts, out_len=lens, out=out, out_descs=rdescs, out_results=rres,
                 index=ridx, used=rused)
 

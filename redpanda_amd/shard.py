@@ -18,7 +18,7 @@ from __future__ import annotations
 import numpy as np
 
 # per-partition summary columns (int64)
-FIELDS = ("batches", "ok", "records", "wire_bytes", "last_offset", "crc_sum", "verdict_mask")
+FIELDS = ("batches", "ok", "records", "wire_bytes", "crc_sum", "last_offset")
 NF = len(FIELDS)
 
 
@@ -35,52 +35,36 @@ def batches_range(rank: int, world: int, total: int) -> tuple[int, int]:
 def partition_summaries(results, descs_partition, lo: int, hi: int):
     """Per-partition summaries of one rank's validated batches.
 
-    results: torch uint8 tensor viewed as rpgpu_batch_result rows (n x 64 B)
-    or an int32 view (n x 16); descs_partition: int64 tensor of each batch's
-    partition id (same device).  Returns an int64 tensor (hi - lo) x NF:
-    batches, OK batches, index entries, wire bytes (size_bytes of OK
-    batches), last offset (max base_offset + last_offset_delta over OK
-    batches, -1 if none), sum of computed CRCs, and a bitmask of the verdict
-    classes seen (bit v for v < 63)."""
+    results: torch uint8 tensor of rpgpu_batch_result rows (n x 64 B, or any
+    view of them); descs_partition: int64 tensor of each batch's partition id
+    (same device).  Returns an int64 tensor (hi - lo) x NF: batches, OK
+    batches, index entries, bytes of OK batches (size_bytes), sum of the
+    computed CRCs, and the last offset (max base_offset + last_offset_delta
+    over OK batches, -1 if none) -- one index_add and one scatter_reduce."""
     import torch
 
-    r = results.view(torch.int32).view(-1, 16)
+    r = results.reshape(-1).view(torch.int32).view(-1, 16)
     n = r.shape[0]
     dev = r.device
     P = hi - lo
     part = descs_partition.to(torch.int64) - lo
-    if n and (int(part.min()) < 0 or int(part.max()) >= P):
-        raise ValueError("a batch lies outside this rank's partition range")
-    verdict = r[:, 0].to(torch.int64)
-    ok = verdict == 0
-    crc = r[:, 1].to(torch.int64) & 0xFFFFFFFF
-    size = r[:, 4].to(torch.int64)
-    base = r[:, 6].to(torch.int64) & 0xFFFFFFFF | (r[:, 7].to(torch.int64) << 32)
-    lod = r[:, 8].to(torch.int64)
-    count = r[:, 15].to(torch.int64) & 0xFFFFFFFF
+    ok = r[:, 0] == 0
+    okl = ok.to(torch.int64)
+    vals = torch.stack([torch.ones(n, dtype=torch.int64, device=dev), okl,
+                        r[:, 15].to(torch.int64) & 0xFFFFFFFF,
+                        r[:, 4].to(torch.int64) * okl,
+                        r[:, 1].to(torch.int64) & 0xFFFFFFFF], dim=1)
     out = torch.zeros(P, NF, dtype=torch.int64, device=dev)
-    one = torch.ones(n, dtype=torch.int64, device=dev)
-    out[:, 0].index_add_(0, part, one)
-    out[:, 1].index_add_(0, part, ok.to(torch.int64))
-    out[:, 2].index_add_(0, part, count)
-    out[:, 3].index_add_(0, part, torch.where(ok, size, torch.zeros_like(size)))
-    last = torch.where(ok, base + lod, torch.full_like(base, -1))
-    out[:, 4] = -1
-    out[:, 4].scatter_reduce_(0, part, last, reduce="amax", include_self=True)
-    out[:, 5].index_add_(0, part, crc)
-    bit = torch.bitwise_left_shift(torch.ones_like(verdict), verdict.clamp(0, 62))
-    # OR-reduce per partition: sum of distinct bits (bit-per-verdict presence)
-    pres = torch.zeros(P, 63, dtype=torch.int64, device=dev)
-    pres.index_put_((part, verdict.clamp(0, 62)), one, accumulate=True)
-    w = torch.bitwise_left_shift(torch.ones(63, dtype=torch.int64, device=dev),
-                                 torch.arange(63, device=dev))
-    out[:, 6] = ((pres > 0).to(torch.int64) * w).sum(dim=1)
-    del bit
+    out[:, :5].index_add_(0, part, vals)
+    base = (r[:, 6].to(torch.int64) & 0xFFFFFFFF) | (r[:, 7].to(torch.int64) << 32)
+    last = torch.where(ok, base + r[:, 8].to(torch.int64), torch.full_like(base, -1))
+    out[:, 5] = -1
+    out[:, 5].scatter_reduce_(0, part, last, reduce="amax", include_self=True)
     return out
 
 
 def gather_summaries(local, world: int, partitions: int):
-    """All-gather every rank's summaries; returns the partitions x NF table on
+    """All-gather every rank's summaries; returns the partitions x columns table on
     every rank (rank g's rows land at its own partition range).  Ranges are
     unequal when G does not divide P, so each rank pads to the largest."""
     import torch
@@ -89,11 +73,12 @@ def gather_summaries(local, world: int, partitions: int):
     if world == 1:
         return local
     width = max(hi - lo for lo, hi in (partition_range(g, world, partitions) for g in range(world)))
-    pad = torch.zeros(width, NF, dtype=torch.int64, device=local.device)
+    nf = local.shape[1]
+    pad = torch.zeros(width, nf, dtype=torch.int64, device=local.device)
     pad[: local.shape[0]] = local
-    allp = torch.empty(world * width, NF, dtype=torch.int64, device=local.device)
+    allp = torch.empty(world * width, nf, dtype=torch.int64, device=local.device)
     dist.all_gather_into_tensor(allp, pad)
-    out = torch.empty(partitions, NF, dtype=torch.int64, device=local.device)
+    out = torch.empty(partitions, nf, dtype=torch.int64, device=local.device)
     for g in range(world):
         lo, hi = partition_range(g, world, partitions)
         out[lo:hi] = allp[g * width: g * width + (hi - lo)]
@@ -104,16 +89,14 @@ def summaries_numpy(results: np.ndarray, partition: np.ndarray, lo: int, hi: int
     """Reference computation of partition_summaries in numpy (for tests)."""
     P = hi - lo
     out = np.zeros((P, NF), dtype=np.int64)
-    out[:, 4] = -1
+    out[:, 5] = -1
     for i in range(len(results)):
         p = int(partition[i]) - lo
-        v = int(results["verdict"][i])
         out[p, 0] += 1
         out[p, 2] += int(results["index_count"][i])
-        out[p, 5] += int(results["crc"][i])
-        out[p, 6] |= 1 << min(max(v, 0), 62)
-        if v == 0:
+        out[p, 4] += int(results["crc"][i])
+        if int(results["verdict"][i]) == 0:
             out[p, 1] += 1
             out[p, 3] += int(results["size_bytes"][i])
-            out[p, 4] = max(out[p, 4], int(results["base_offset"][i]) + int(results["last_offset_delta"][i]))
+            out[p, 5] = max(out[p, 5], int(results["base_offset"][i]) + int(results["last_offset_delta"][i]))
     return out
