@@ -217,7 +217,6 @@ def main() -> int:
         f"{time.perf_counter() - t_gen:.1f}s, H2D {h2d_bytes / max(h2d_time, 1e-9) / 1e9:.1f} GB/s")
 
     d_descs = torch.from_numpy(descs.view(np.uint8)).to(dev)
-    d_part = torch.from_numpy(descs["partition"].astype(np.int64)).to(dev)
     d_res = torch.zeros(n * 64, dtype=torch.uint8, device=dev)
     d_scratch = torch.zeros(engine.Engine.scratch_bytes(n), dtype=torch.uint8, device=dev)
     d_used = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -273,9 +272,10 @@ def main() -> int:
             run_events.append((e0, e1))
         # the final gather: per-partition summaries of this rank's range (for
         # the decompress configs, of the input batches and the rewritten ones)
-        s = shard.partition_summaries(d_res, d_part, plo, phi)
+        s = shard.partition_summaries_device(eng, d_descs, d_res, n, plo, phi, sh)
         if decompress:
-            s = torch.cat([s, shard.partition_summaries(d_ores, d_part, plo, phi)], dim=1)
+            # the rewritten batches carry the same partition ids (rpgpu_decomp_run_device)
+            s = torch.cat([s, shard.partition_summaries_device(eng, d_odescs, d_ores, n, plo, phi, sh)], dim=1)
         table[0] = shard.gather_summaries(s, world, P_total)
 
     for _ in range(args.warmup):

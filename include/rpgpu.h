@@ -428,6 +428,18 @@ int32_t rpgpu_segment_index_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_des
                                    uint32_t nsegs, rpgpu_segment_state* d_states,
                                    rpgpu_index_entry* d_entries, void* hip_stream);
 
+/* ---- partition summaries (multi-GPU gather) -------------------------------
+ * Per partition p of [part_lo, part_lo + nparts), over the batches of
+ * d_descs / d_results (a validation's output; batches of other partitions
+ * are ignored), six int64 columns at d_out[p * 6]: batches, OK batches,
+ * index entries, bytes of OK batches (size_bytes), sum of the computed CRCs,
+ * and the last offset (max base_offset + last_offset_delta over OK batches,
+ * -1 if none; storage/offset_assignment.h:25-28).  A partition-sharded run
+ * (one GPU per partition range) gathers these to one rank. */
+int32_t rpgpu_partition_summaries_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_descs,
+                                         const rpgpu_batch_result* d_results, uint32_t n, uint32_t part_lo,
+                                         uint32_t nparts, int64_t* d_out, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

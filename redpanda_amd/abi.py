@@ -184,6 +184,7 @@ def lib() -> C.CDLL:
         _sig(L.rpgpu_eventfd, C.c_int, _vp)
         _sig(L.rpgpu_kafka_error_code, _i32, _vp, _u32)
         _sig(L.rpgpu_kafka_error_codes_device, _i32, _vp, _vp, _u32, _u32, _vp, _vp)
+        _sig(L.rpgpu_partition_summaries_device, _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
         if not hasattr(L, "rpgpu_decomp_scratch_bytes"):  # an older build (A/B timing runs)
             _LIB = L
             return _LIB
@@ -221,6 +222,7 @@ EXPORTED = [
     "rpgpu_abi_version", "rpgpu_open", "rpgpu_close", "rpgpu_last_error", "rpgpu_device_info",
     "rpgpu_arena_alloc", "rpgpu_arena_free", "rpgpu_submit", "rpgpu_poll", "rpgpu_wait",
     "rpgpu_eventfd", "rpgpu_kafka_error_code", "rpgpu_kafka_error_codes_device",
+    "rpgpu_partition_summaries_device",
     "rpgpu_validate_scratch_bytes", "rpgpu_validate_device", "rpgpu_plan_device",
     "rpgpu_run_device", "rpgpu_crc32c_ranges_device",
     "rpgpu_crc32c_extend", "rpgpu_internal_header_only_crc", "rpgpu_crc_record_batch",

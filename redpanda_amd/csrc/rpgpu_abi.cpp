@@ -63,6 +63,8 @@ hipError_t launch_uncompress_one(uint32_t codec, const uint8_t* d_in, uint64_t n
                                  uint64_t* d_res, hipStream_t s);
 hipError_t launch_kafka_codes(const rpgpu_batch_result* d_res, uint32_t n, uint32_t batch_max_bytes,
                               int32_t* d_codes, hipStream_t s);
+hipError_t launch_summaries(const rpgpu_batch_desc* d_descs, const rpgpu_batch_result* d_res, uint32_t n,
+                            uint32_t part_lo, uint32_t nparts, int64_t* d_out, hipStream_t s);
 }  // namespace rpgpu
 
 namespace {
@@ -231,6 +233,16 @@ int rpgpu_eventfd(rpgpu_ctx* c) { return c ? c->efd : -1; }
 int32_t rpgpu_kafka_error_code(const rpgpu_batch_result* r, uint32_t batch_max_bytes) {
     if (!r) return RPGPU_KAFKA_ERR_UNKNOWN_SERVER_ERROR;
     return rpgpu::kafka_error_code(r->verdict, r->size_bytes, batch_max_bytes);
+}
+
+int32_t rpgpu_partition_summaries_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs,
+                                         const rpgpu_batch_result* d_results, uint32_t n, uint32_t part_lo,
+                                         uint32_t nparts, int64_t* d_out, void* hip_stream) {
+    if (!c || (n && (!d_descs || !d_results)) || (nparts && !d_out)) return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_summaries(d_descs, d_results, n, part_lo, nparts, d_out, s);
+    if (e != hipSuccess) return fail(c, e, "summaries launch");
+    return RPGPU_OK;
 }
 
 int32_t rpgpu_kafka_error_codes_device(rpgpu_ctx* c, const rpgpu_batch_result* d_results, uint32_t n,

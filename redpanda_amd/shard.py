@@ -32,6 +32,22 @@ def batches_range(rank: int, world: int, total: int) -> tuple[int, int]:
     return total * rank // world, total * (rank + 1) // world
 
 
+def partition_summaries_device(eng, d_descs, d_results, n: int, lo: int, hi: int, stream: int = 0):
+    """partition_summaries on the GPU (rpgpu_partition_summaries_device): d_descs
+    / d_results are device tensors of the arena's descriptors and results."""
+    import torch
+
+    from . import abi
+    from .engine import EngineError
+
+    out = torch.empty(hi - lo, NF, dtype=torch.int64, device=d_results.device)
+    rc = abi.lib().rpgpu_partition_summaries_device(eng.ctx, d_descs.data_ptr(), d_results.data_ptr(), n, lo,
+                                                    hi - lo, out.data_ptr(), stream or None)
+    if rc != abi.RPGPU_OK:
+        raise EngineError(f"rpgpu_partition_summaries_device: {rc} {eng.last_error()}")
+    return out
+
+
 def partition_summaries(results, descs_partition, lo: int, hi: int):
     """Per-partition summaries of one rank's validated batches.
 
