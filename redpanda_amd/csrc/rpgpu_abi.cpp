@@ -60,7 +60,8 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
 hipError_t launch_uncompress_bound(uint32_t codec, const uint8_t* d_in, uint64_t n, uint64_t* d_res,
                                    hipStream_t s);
 hipError_t launch_uncompress_one(uint32_t codec, const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint64_t cap,
-                                 uint64_t* d_res, hipStream_t s);
+                                 uint64_t* d_res, uint8_t* d_lits, hipStream_t s);
+size_t uncompress_scratch_bytes();
 hipError_t launch_kafka_codes(const rpgpu_batch_result* d_res, uint32_t n, uint32_t batch_max_bytes,
                               int32_t* d_codes, hipStream_t s);
 hipError_t launch_summaries(const rpgpu_batch_desc* d_descs, const rpgpu_batch_result* d_res, uint32_t n,
@@ -567,9 +568,12 @@ int32_t rpgpu_uncompress(rpgpu_ctx* c, int32_t codec, const void* in, size_t n, 
         *out_len = bound;
         return RPGPU_V_DECOMP_OVERFLOW;
     }
-    if ((e = c->small_out.reserve(bound + 256)) != hipSuccess) return fail(c, e, "device buffer");
+    const size_t o_lits = align_up(bound + 256, 256);
+    if ((e = c->small_out.reserve(o_lits + rpgpu::uncompress_scratch_bytes())) != hipSuccess)
+        return fail(c, e, "device buffer");
     uint8_t* dout = static_cast<uint8_t*>(c->small_out.p);
-    if ((e = rpgpu::launch_uncompress_one((uint32_t)codec, base, n, dout, bound, meta, c->stream)) != hipSuccess)
+    if ((e = rpgpu::launch_uncompress_one((uint32_t)codec, base, n, dout, bound, meta, dout + o_lits, c->stream)) !=
+        hipSuccess)
         return fail(c, e, "uncompress launch");
     if ((e = hipMemcpyAsync(h, meta, sizeof(h), hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(c->stream)) != hipSuccess)

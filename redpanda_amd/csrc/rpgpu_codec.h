@@ -15,13 +15,14 @@
 //          snappy::GetUncompressedLength / snappy::RawUncompress (snappy 1.1.8)
 //   dispatch compression/compression.cc:35-55
 //
-// Plain C++: the same code runs on the device (rpgpu_decomp.hip) and on the
-// host in the differential fuzz test against the oracle
-// (tests/native/codec_fuzz.cpp).  Copies move up to 64 bytes per step and may
-// run up to 63 bytes past the end of a sequence (later sequences overwrite
-// those bytes, as liblz4's own wild copies do), so an output buffer needs
-// kSlack writable bytes past its planned capacity and an input buffer 64
-// readable bytes past its end (RPGPU_ARENA_TAIL_PAD).
+// Plain C++: the same decision code runs on the device (rpgpu_decomp.hip,
+// executed uniformly by a wavefront whose emitter runs the copies with all
+// lanes, rpgpu_wave.h) and on the host in the differential fuzz test against
+// the oracle (tests/native/codec_fuzz.cpp, DirectEmit).  Direct copies move up
+// to 64 bytes per step and may run up to 63 bytes past the end of a sequence
+// (later sequences overwrite those bytes, as liblz4's own wild copies do), so
+// an output buffer needs kSlack writable bytes past its planned capacity and
+// an input buffer 64 readable bytes past its end (RPGPU_ARENA_TAIL_PAD).
 #ifndef RPGPU_CODEC_H
 #define RPGPU_CODEC_H
 
@@ -42,9 +43,9 @@ constexpr uint64_t kMaxChunk = 128u * 1024u;  // details::io_allocation_size::ma
 constexpr int32_t V_OK = 0, V_UNDEFINED = 11, V_ERROR = 30, V_TRAILING = 32, V_UNSUPPORTED = 33,
                   V_OVERFLOW = 34;
 
-struct B16 {
-    uint32_t w[4];
-};
+// 16 bytes as a vector value (a struct with an array member would be kept in
+// scratch memory by the device compiler when live across branches)
+typedef uint32_t B16 __attribute__((vector_size(16)));
 RPC_HD void ld16(B16& v, const uint8_t* p) { __builtin_memcpy(&v, p, 16); }
 RPC_HD void st16(uint8_t* p, const B16& v) { __builtin_memcpy(p, &v, 16); }
 RPC_HD uint32_t le16(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
@@ -129,12 +130,24 @@ RPC_HD void copy_match(uint8_t* dst, uint64_t off, uint64_t n) {
         step = off * (16 / off);  // a whole number of periods
     }
     B16 p;
-    p.w[0] = (uint32_t)lo;
-    p.w[1] = (uint32_t)(lo >> 32);
-    p.w[2] = (uint32_t)hi;
-    p.w[3] = (uint32_t)(hi >> 32);
+    p[0] = (uint32_t)lo;
+    p[1] = (uint32_t)(lo >> 32);
+    p[2] = (uint32_t)hi;
+    p[3] = (uint32_t)(hi >> 32);
     for (uint64_t i = 0; i < n; i += step) st16(dst + i, p);
 }
+
+// ---------------------------------------------------------------- emitters
+// The decoders below decide everything -- acceptance, lengths, offsets --
+// from the input alone and hand every literal run and back-reference to an
+// emitter.  DirectEmit copies at once (the host fuzz build, wild copies
+// within kSlack); the device's wave-cooperative emitter (rpgpu_wave.h)
+// collects 64 sequences and executes them with the whole wavefront.
+struct DirectEmit {
+    RPC_HD void lits(uint8_t* dst, const uint8_t* src, uint64_t n) { copy_fwd(dst, src, n); }
+    RPC_HD void match(uint8_t* dst, uint64_t off, uint64_t n) { copy_match(dst, off, n); }
+    RPC_HD void sync() {}
+};
 
 // ---------------------------------------------------------------- input window
 // The decoders read tokens, lengths and offsets through 32 bytes of input
@@ -150,8 +163,8 @@ RPC_HD void win_load(InWin& W, const uint8_t* in, int64_t p) {
     B16 a, b;
     ld16(a, in + p);
     ld16(b, in + p + 16);
-    W.w0 = a.w[0], W.w1 = a.w[1], W.w2 = a.w[2], W.w3 = a.w[3];
-    W.w4 = b.w[0], W.w5 = b.w[1], W.w6 = b.w[2], W.w7 = b.w[3];
+    W.w0 = a[0], W.w1 = a[1], W.w2 = a[2], W.w3 = a[3];
+    W.w4 = b[0], W.w5 = b[1], W.w6 = b[2], W.w7 = b[3];
     W.pos = p;
 }
 // dword q (0..8; 8 reads as 0) of the window: selects, not an indexed array
@@ -245,7 +258,8 @@ RPC_HD uint32_t lz4_varlen(InWin& W, const uint8_t* in, int64_t& ip, int64_t len
 // `hist` = bytes of earlier frame output before `out` that matches may reach
 // (linked blocks; LZ4F keeps at least min(history, 64 KiB) as dictionary).
 // Returns the decoded size, or -1.
-RPC_HD int64_t lz4_block(const uint8_t* in, int64_t isz, uint8_t* out, int64_t ocap, int64_t hist) {
+template <class E>
+RPC_HD int64_t lz4_block(E& em, const uint8_t* in, int64_t isz, uint8_t* out, int64_t ocap, int64_t hist) {
     if (isz == 0) return -1;  // ocap (maxBlockSize) is never 0 here
     const int64_t iend = isz, oend = ocap;
     const bool check_off = hist < 65536;  // checkOffset: dictSize < 64 KB
@@ -271,14 +285,14 @@ RPC_HD int64_t lz4_block(const uint8_t* in, int64_t isz, uint8_t* out, int64_t o
         } else {
             // two-stage shortcut: literal length 0..14 and room for 16 + 18 bytes
             if (len != 15 && ip < iend - 16 && op <= oend - 32) {
-                copy_fwd(out + op, in + ip, (uint64_t)len);
+                em.lits(out + op, in + ip, (uint64_t)len);
                 op += len;
                 ip += len;
                 len = token & 15;
                 off = win_at(W, in, ip, 2) & 0xFFFFu;
                 ip += 2;
                 if (len != 15 && off >= 8 && off <= op + hist) {  // match >= lowPrefix
-                    copy_match(out + op, (uint64_t)off, (uint64_t)len + 4);
+                    em.match(out + op, (uint64_t)off, (uint64_t)len + 4);
                     op += len + 4;
                     continue;
                 }
@@ -293,10 +307,10 @@ RPC_HD int64_t lz4_block(const uint8_t* in, int64_t isz, uint8_t* out, int64_t o
         if (lit_checks && (op + len > oend - 12 || ip + len > iend - 8)) {
             // MFLIMIT / input parsing restriction: must be the last literals
             if (ip + len != iend || op + len > oend) return -1;
-            copy_fwd(out + op, in + ip, (uint64_t)len);
+            em.lits(out + op, in + ip, (uint64_t)len);
             return op + len;
         }
-        copy_fwd(out + op, in + ip, (uint64_t)len);
+        em.lits(out + op, in + ip, (uint64_t)len);
         ip += len;
         op += len;
         off = win_at(W, in, ip, 2) & 0xFFFFu;
@@ -311,7 +325,7 @@ RPC_HD int64_t lz4_block(const uint8_t* in, int64_t isz, uint8_t* out, int64_t o
         if (!safe && op + len >= oend - 64) safe = true;  // goto safe_match_copy
         if (check_off && off > op + hist) return -1;      // offset outside buffers
         if (safe && op + len > oend - 5) return -1;       // last LASTLITERALS bytes are literals
-        copy_match(out + op, (uint64_t)off, (uint64_t)len);
+        em.match(out + op, (uint64_t)off, (uint64_t)len);
         op += len;
     }
 }
@@ -401,7 +415,8 @@ RPC_HD uint64_t lz4_chunk_end(uint64_t first, uint64_t s) {
 // the end of the input and was decoded into LZ4F's tmpOut (less than
 // maxBlockSize of room left in the chunk) is flushed only as far as the
 // chunk has room, and the rest is dropped when the loop exits.
-RPC_HD int32_t lz4f_uncompress(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len) {
+template <class E>
+RPC_HD int32_t lz4f_uncompress(E& em, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len) {
     *out_len = 0;
     const Lz4Frame f = lz4f_header(in, n);
     if (f.kind == kLz4Error) return V_ERROR;
@@ -420,6 +435,7 @@ RPC_HD int32_t lz4f_uncompress(const uint8_t* in, uint64_t n, uint8_t* out, uint
             if (f.content != 0 && o != f.content) return V_ERROR;  // frameSize_wrong
             if (f.content_sum) {
                 if (n - pos < 4) break;
+                em.sync();  // the checksum reads the decoded bytes
                 if (le32(in + pos) != xxh32(out, o, 0)) return V_ERROR;  // contentChecksum_invalid
                 pos += 4;
             }
@@ -434,7 +450,7 @@ RPC_HD int32_t lz4f_uncompress(const uint8_t* in, uint64_t n, uint8_t* out, uint
                 *out_len = o;
                 return V_OVERFLOW;
             }
-            copy_fwd(out + o, in + pos, take);
+            em.lits(out + o, in + pos, take);
             o += take;
             pos += take;
             if (take < size) break;
@@ -452,7 +468,7 @@ RPC_HD int32_t lz4f_uncompress(const uint8_t* in, uint64_t n, uint8_t* out, uint
             *out_len = o;
             return V_OVERFLOW;
         }
-        const int64_t d = lz4_block(in + pos, (int64_t)size, out + o, f.max_block, f.linked ? (int64_t)o : 0);
+        const int64_t d = lz4_block(em, in + pos, (int64_t)size, out + o, f.max_block, f.linked ? (int64_t)o : 0);
         if (d < 0) return V_ERROR;  // decompressionFailed
         const uint64_t s = o;
         o += (uint64_t)d;
@@ -521,7 +537,8 @@ RPC_HD bool snappy_varint(const uint8_t* p, uint64_t n, uint32_t& v, uint32_t& u
 // and the output, a copy must satisfy 0 < offset <= produced and fit the
 // output; success = the input ends at a tag boundary with exactly
 // `expected` bytes produced.
-RPC_HD bool snappy_raw(const uint8_t* in, uint64_t n, uint8_t* out, uint32_t expected, uint32_t hdr) {
+template <class E>
+RPC_HD bool snappy_raw(E& em, const uint8_t* in, uint64_t n, uint8_t* out, uint32_t expected, uint32_t hdr) {
     uint64_t ip = hdr, op = 0;
     InWin W;
     win_load(W, in, (int64_t)ip);
@@ -543,7 +560,7 @@ RPC_HD bool snappy_raw(const uint8_t* in, uint64_t n, uint8_t* out, uint32_t exp
             }
             if (n - ip < len) return false;        // premature end of input
             if (op + len > expected) return false;  // SnappyArrayWriter::Append
-            copy_fwd(out + op, in + ip, len);
+            em.lits(out + op, in + ip, len);
             op += len;
             ip += len;
         } else {
@@ -561,7 +578,7 @@ RPC_HD bool snappy_raw(const uint8_t* in, uint64_t n, uint8_t* out, uint32_t exp
             ip += extra;
             if (off == 0 || op < off) return false;  // Produced() <= offset - 1u
             if (op + len > expected) return false;
-            copy_match(out + op, off, len);
+            em.match(out + op, off, len);
             op += len;
         }
     }
@@ -571,13 +588,14 @@ RPC_HD bool snappy_raw(const uint8_t* in, uint64_t n, uint8_t* out, uint32_t exp
 // calls it (oracle/codec.c snappy_raw_append): the length preamble, then a
 // raw decode of exactly that many bytes.  zero_skip: a 0-length preamble
 // yields nothing without looking further (the unframed path, :152-160).
-RPC_HD int32_t snappy_raw_append(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t& o,
+template <class E>
+RPC_HD int32_t snappy_raw_append(E& em, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t& o,
                                  bool zero_skip) {
     uint32_t ulen, used;
     if (!snappy_varint(in, n, ulen, used)) return V_ERROR;
     if (zero_skip && ulen == 0) return V_OK;
     if (o + ulen > cap) return V_OVERFLOW;
-    if (!snappy_raw(in, n, out + o, ulen, used)) return V_ERROR;
+    if (!snappy_raw(em, in, n, out + o, ulen, used)) return V_ERROR;
     o += ulen;
     return V_OK;
 }
@@ -590,12 +608,13 @@ RPC_HD bool snappy_java_magic(const uint8_t* x) {
 // snappy_java_compressor::uncompress (snappy_java_compressor.cc:76-110):
 // < 16 bytes or no magic -> raw snappy of the whole buffer; else the LE
 // min_version check and {BE i32 length, raw chunk} until the input is used.
-RPC_HD int32_t snappy_java_uncompress(const uint8_t* x, uint64_t n, uint8_t* out, uint64_t cap,
+template <class E>
+RPC_HD int32_t snappy_java_uncompress(E& em, const uint8_t* x, uint64_t n, uint8_t* out, uint64_t cap,
                                       uint64_t* out_len) {
     uint64_t o = 0;
     int32_t v = V_OK;
     if (n < 16 || !snappy_java_magic(x)) {
-        v = snappy_raw_append(x, n, out, cap, o, true);
+        v = snappy_raw_append(em, x, n, out, cap, o, true);
         *out_len = o;
         return v;
     }
@@ -615,7 +634,7 @@ RPC_HD int32_t snappy_java_uncompress(const uint8_t* x, uint64_t n, uint8_t* out
             break;
         }
         const uint64_t take = (uint64_t)clen < n - pos ? (uint64_t)clen : n - pos;  // short copy
-        v = snappy_raw_append(x + pos, take, out, cap, o, false);
+        v = snappy_raw_append(em, x + pos, take, out, cap, o, false);
         if (v != V_OK) break;
         pos += take;
     }
@@ -644,15 +663,16 @@ RPC_HD uint64_t snappy_java_bound(const uint8_t* x, uint64_t n) {
 }
 
 // ---------------------------------------------------------------- dispatch
-// compression::compressor::uncompress (compression.cc:35-55).  gzip (1) and
-// zstd (4) are not decoded by this engine yet: RPGPU_V_DECOMP_UNSUPPORTED.
-RPC_HD int32_t uncompress(uint32_t codec, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap,
+// compression::compressor::uncompress (compression.cc:35-55) for snappy and
+// LZ4; zstd (4) is rpgpu_zstd.h's, gzip (1) rpgpu_inflate.h's.
+template <class E>
+RPC_HD int32_t uncompress(E& em, uint32_t codec, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap,
                           uint64_t* out_len) {
     *out_len = 0;
     if (n == 0) return V_ERROR;  // "Asked to decompress an empty buffer"
     switch (codec) {
-    case 2: return snappy_java_uncompress(in, n, out, cap, out_len);
-    case 3: return lz4f_uncompress(in, n, out, cap, out_len);
+    case 2: return snappy_java_uncompress(em, in, n, out, cap, out_len);
+    case 3: return lz4f_uncompress(em, in, n, out, cap, out_len);
     case 1:
     case 4: return V_UNSUPPORTED;
     default: return V_ERROR;  // none: "nothing to uncompress"

@@ -2,7 +2,7 @@
 //
 // Replaces, per batch, compression::compressor::uncompress
 // (compression/compression.cc:35-55 and the codec wrappers restated in
-// rpgpu_codec.h) and the rewrite of storage::internal::
+// rpgpu_codec.h / rpgpu_zstd.h) and the rewrite of storage::internal::
 // maybe_decompress_batch_sync (storage/parser_utils.cc:52-68,122-128): the
 // decompressed body becomes a new on-disk batch with the codec bits removed,
 // size_bytes = 61 + body, crc = crc_record_batch over the decompressed body
@@ -14,22 +14,19 @@
 //                        61-byte header + an upper bound of the decoded size
 //                        read off the frame's block headers / chunk
 //                        preambles + kSlack; exclusive scan of the slots
-//   decomp_kernel        one lane per batch decodes its body into its slot
-//                        and writes the rewritten header (CRC fields 0) and
-//                        the rewritten batch's descriptor
+//   decomp_wave_kernel   one wavefront per batch (persistent grid, batches
+//                        taken from an atomic counter): the codec's decisions
+//                        run uniformly in all lanes, the bytes are produced
+//                        by the wave 64 sequences at a time (rpgpu_wave.h);
+//                        zstd's Huffman / FSE tables live in LDS
 //   validate_kernel      over the rewritten batches with RPGPU_OP_RECRC: the
 //                        Kafka CRC of the decompressed body, then the header
 //                        CRC over the header carrying it; record walk; index
 //   decomp_patch_kernel  stores both CRCs into the rewritten headers
-// Decoding is one lane per batch: an LZ4 or snappy stream is a chain of
-// dependent sequences, and with every batch of an arena in flight at once
-// (C3: 262,144 lanes, 16 waves per CU) the chip is filled with batches
-// rather than by splitting one stream.  zstd batches (codec 4) go to
-// zstd_kernel instead: also one lane per batch, each with its own Huffman /
-// FSE workspace (rpzstd::Ws, ~19 KB) in HBM (rpgpu_zstd.h).
 #include "rpgpu_device.h"  // before rpgpu_codec.h: HIP attributes
 #include "rpgpu_codec.h"
 #include "rpgpu_zstd.h"
+#include "rpgpu_wave.h"
 
 namespace rpgpu {
 
@@ -43,23 +40,24 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
 size_t validate_scratch_bytes(uint32_t n);
 
 namespace {
-// zstd decoders in flight at once (one lane each), and so per-lane workspaces
-#ifndef RPZ_LANES
-#define RPZ_LANES 131072  // 2 waves per SIMD at the kernel's VGPR count
-#endif
-constexpr uint32_t kZstdLanes = RPZ_LANES;
-uint32_t zstd_lanes(uint32_t n) { return n < kZstdLanes ? n : kZstdLanes; }
-// scratch: slot[n] u64 | local[n] u64 | block_sum[nb] u64 | validate scratch | zstd Ws[lanes]
+// decoder wavefronts in flight: 8 per CU (the zstd workspace takes ~19 KB of
+// the 160 KiB LDS) on 256 CUs; each owns a literal scratch buffer
+constexpr uint32_t kDecompWaves = 2048;
+constexpr uint64_t kLitScratch = (128u << 10) + 256;  // ZSTD_BLOCKSIZE_MAX + slack
+uint32_t decomp_waves(uint32_t n) { return n < kDecompWaves ? n : kDecompWaves; }
+// scratch: slot[n] u64 | local[n] u64 | block_sum[nb] u64 | validate scratch |
+//          counter (256 B) | literal scratch[waves]
 struct Parts {
     uint64_t *slot, *local, *block_sum;
     void* vscratch;
-    rpzstd::Ws* zws;
+    uint32_t* counter;
+    uint8_t* lits;
 };
 size_t parts_head(uint32_t n) {
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
     return ((size_t)n * 16 + nb * 8 + 255) & ~(size_t)255;
 }
-size_t zws_offset(uint32_t n) { return (parts_head(n) + validate_scratch_bytes(n) + 255) & ~(size_t)255; }
+size_t counter_offset(uint32_t n) { return (parts_head(n) + validate_scratch_bytes(n) + 255) & ~(size_t)255; }
 Parts parts(void* p, uint32_t n) {
     uint8_t* b = static_cast<uint8_t*>(p);
     Parts s;
@@ -67,12 +65,13 @@ Parts parts(void* p, uint32_t n) {
     s.local = s.slot + n;
     s.block_sum = s.local + n;
     s.vscratch = b + parts_head(n);
-    s.zws = reinterpret_cast<rpzstd::Ws*>(b + zws_offset(n));
+    s.counter = reinterpret_cast<uint32_t*>(b + counter_offset(n));
+    s.lits = b + counter_offset(n) + 256;
     return s;
 }
 }  // namespace
 
-size_t decomp_scratch_bytes(uint32_t n) { return zws_offset(n) + (size_t)zstd_lanes(n) * sizeof(rpzstd::Ws); }
+size_t decomp_scratch_bytes(uint32_t n) { return counter_offset(n) + 256 + (size_t)decomp_waves(n) * kLitScratch; }
 
 // slot[i] of a batch whose bound exceeds the per-batch ceiling: no output
 // reserved (the scan counts 0), verdict DECOMP_OVERFLOW
@@ -186,90 +185,71 @@ __device__ __forceinline__ void finish_batch(uint32_t i, const rpgpu_batch_desc&
     out_descs[i] = od;
 }
 
-__global__ __launch_bounds__(256) void decomp_kernel(
-    const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
-    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
-    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
-    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
-    rpgpu_batch_desc* __restrict__ out_descs) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const rpgpu_batch_desc d = descs[i];
-    const rpgpu_batch_result v = vres[i];
-    const bool want = decomp_wanted(d, v);
-    if (want && v.codec == 4) return;  // zstd_kernel
-    const uint64_t off = block_base[i / kScanBlock] + local[i];
-    uint64_t sz = slot[i];
-    int32_t verdict = RPGPU_V_SKIPPED;
-    uint64_t len = 0;
-    if (want) {
-        if (sz == kOverCeiling) {
-            sz = 0;
-            verdict = RPGPU_V_DECOMP_OVERFLOW;
-        } else if (sz == 0) {
-            verdict = RPGPU_V_DECOMP_UNSUPPORTED;  // gzip
-        } else if (off + sz > out_cap) {
-            verdict = RPGPU_V_DECOMP_OVERFLOW;  // caller's buffer smaller than the plan
-        } else {
-            const uint8_t* p = data + d.offset;
-            verdict = rpcodec::uncompress(v.codec, p + kHeaderSize, (uint64_t)(uint32_t)v.size_bytes - kHeaderSize,
-                                          out + off + kHeaderSize, sz - kHeaderSize - rpcodec::kSlack, &len);
-        }
+// One batch body through the codec restatement, bytes produced by the wave.
+// K: the codec family a kernel instance decodes (kFamZstd: 4, kFamLz: 2 and 3).
+constexpr uint32_t kFamZstd = 4, kFamLz = 3;
+__device__ __forceinline__ bool in_family(uint32_t fam, uint32_t codec) {
+    return fam == kFamZstd ? codec == 4 : (codec == 2 || codec == 3);
+}
+template <uint32_t FAM>
+__device__ __forceinline__ int32_t decode_body(rpwave::WaveEmit& em, rpzstd::Ws& ws, uint32_t codec, const uint8_t* in,
+                                               uint64_t n, uint8_t* out, uint64_t cap, uint64_t* len) {
+    int32_t v;
+    if (FAM == kFamZstd) {
+        v = rpzstd::uncompress(em, in, n, out, cap, len, ws);
+    } else {
+        v = rpcodec::uncompress(em, codec, in, n, out, cap, len);
+        em.sync();
     }
-    finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
+    return v;
 }
 
-// zstd batches: one lane per batch (grid-stride over kZstdLanes lanes), each
-// with its own workspace (Huffman / FSE tables) in HBM.  The decode is a chain
-// of dependent loads per symbol and per sequence; what hides that latency is
-// the number of frames in flight, so tables live where every lane can have
-// its own rather than in LDS (~19 KB per frame caps LDS at 8 frames per CU).
-#ifndef RPZ_MIN_WAVES
-#define RPZ_MIN_WAVES 1
-#endif
-__global__ __launch_bounds__(256, RPZ_MIN_WAVES) void zstd_kernel(
+// One wavefront per batch over a persistent grid of kDecompWaves waves; each
+// wave takes the next batch from an atomic counter (skewed batch sizes: a
+// wave that drew a 1 MiB body does not hold up the batches queued behind
+// it).  The zstd workspace is the wave's LDS.
+template <uint32_t FAM>
+__global__ __launch_bounds__(64) void decomp_wave_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
     const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
-    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
-    rpgpu_batch_desc* __restrict__ out_descs, rpzstd::Ws* __restrict__ wsbuf) {
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t lanes = gridDim.x * blockDim.x;
-    if (g >= n) return;  // lanes past the arena own no workspace
-    rpzstd::Ws& ws = wsbuf[g];
-#if RPZ_PROF
-    const uint64_t k0 = RPZ_CLK();
-    uint32_t nb_done = 0;
-    ws.t_lit = ws.t_seq = ws.n_seq = ws.n_lit = 0;
-#endif
-    for (uint32_t i = g; i < n; i += lanes) {
+    rpgpu_decomp_result* __restrict__ dres, uint8_t* out, uint64_t out_cap,
+    rpgpu_batch_desc* __restrict__ out_descs, uint32_t* counter, uint8_t* lit_scratch) {
+    __shared__ rpzstd::Ws ws;
+    const uint32_t lid = lane_id();
+    rpwave::WaveEmit em;
+    em.init(lit_scratch + (uint64_t)blockIdx.x * kLitScratch);
+    for (;;) {
+        uint32_t i = 0;
+        if (lid == 0) i = atomicAdd(counter, 1u);
+        i = __builtin_amdgcn_readfirstlane(i);
+        if (i >= n) break;
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
-        if (!decomp_wanted(d, v) || v.codec != 4) continue;
+        const bool want = decomp_wanted(d, v);
+        // each batch has one owner: zstd batches the zstd instance, every
+        // other batch (LZ4, snappy, gzip, skipped) the LZ instance
+        if (FAM == kFamZstd ? !(want && v.codec == 4) : (want && v.codec == 4)) continue;
         const uint64_t off = block_base[i / kScanBlock] + local[i];
         uint64_t sz = slot[i];
-        int32_t verdict;
+        int32_t verdict = RPGPU_V_SKIPPED;
         uint64_t len = 0;
-        if (sz == kOverCeiling) {
-            sz = 0;
-            verdict = RPGPU_V_DECOMP_OVERFLOW;
-        } else if (off + sz > out_cap) {
-            verdict = RPGPU_V_DECOMP_OVERFLOW;
-        } else {
-            verdict = rpzstd::uncompress(data + d.offset + kHeaderSize, (uint64_t)(uint32_t)v.size_bytes - kHeaderSize,
-                                         out + off + kHeaderSize, sz - kHeaderSize - rpcodec::kSlack, &len, ws);
+        if (want) {
+            if (sz == kOverCeiling) {
+                sz = 0;
+                verdict = RPGPU_V_DECOMP_OVERFLOW;
+            } else if (sz == 0) {
+                verdict = RPGPU_V_DECOMP_UNSUPPORTED;  // gzip
+            } else if (off + sz > out_cap) {
+                verdict = RPGPU_V_DECOMP_OVERFLOW;  // caller's buffer smaller than the plan
+            } else {
+                verdict = decode_body<FAM>(em, ws, v.codec, data + d.offset + kHeaderSize,
+                                      (uint64_t)(uint32_t)v.size_bytes - kHeaderSize, out + off + kHeaderSize,
+                                      sz - kHeaderSize - rpcodec::kSlack, &len);
+            }
         }
-        finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
-#if RPZ_PROF
-        nb_done++;
-#endif
+        if (lid == 0) finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
     }
-#if RPZ_PROF
-    if (g < 4 || g == (n < lanes ? n : lanes) - 1)  // diagnostics build: phase clocks of a few lanes
-        printf("RPZ_PROF lane=%u batches=%u total=%llu lit=%llu seq=%llu n_lit=%llu n_seq=%llu\n", g, nb_done,
-               (unsigned long long)(RPZ_CLK() - k0), (unsigned long long)ws.t_lit, (unsigned long long)ws.t_seq,
-               (unsigned long long)ws.n_lit, (unsigned long long)ws.n_seq);
-#endif
 }
 
 // stores the CRCs the validation of the rewritten batches computed
@@ -283,18 +263,25 @@ __global__ __launch_bounds__(256) void decomp_patch_kernel(const rpgpu_decomp_re
     put_le(o, 17, vres2[i].crc, 4);
 }
 
-// scalar mirror (rpgpu_uncompress): one lane
+// scalar mirror (rpgpu_uncompress): the bound in one lane, the decode in one wave
 __global__ void uncompress_bound_kernel(uint32_t codec, const uint8_t* in, uint64_t n, uint64_t* res) {
     if (blockIdx.x == 0 && threadIdx.x == 0)
         res[0] = codec == 4 ? (n ? rpzstd::bound(in, n) : 0) : rpcodec::uncompress_bound(codec, in, n);
 }
-__global__ void uncompress_one_kernel(uint32_t codec, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap,
-                                      uint64_t* res) {
+__global__ __launch_bounds__(64) void uncompress_one_kernel(uint32_t codec, const uint8_t* in, uint64_t n,
+                                                            uint8_t* out, uint64_t cap, uint64_t* res,
+                                                            uint8_t* lit_scratch) {
     __shared__ rpzstd::Ws ws;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        uint64_t len = 0;
-        res[1] = (uint64_t)(int64_t)(codec == 4 ? rpzstd::uncompress(in, n, out, cap, &len, ws)
-                                                 : rpcodec::uncompress(codec, in, n, out, cap, &len));
+    rpwave::WaveEmit em;
+    em.init(lit_scratch);
+    uint64_t len = 0;
+    int32_t v;
+    if (n == 0) v = RPGPU_V_DECOMP_ERROR;  // "Asked to decompress an empty buffer"
+    else if (codec == 4) v = decode_body<kFamZstd>(em, ws, codec, in, n, out, cap, &len);
+    else if (codec == 2 || codec == 3) v = decode_body<kFamLz>(em, ws, codec, in, n, out, cap, &len);
+    else v = codec == 1 ? RPGPU_V_DECOMP_UNSUPPORTED : RPGPU_V_DECOMP_ERROR;
+    if (lane_id() == 0) {
+        res[1] = (uint64_t)(int64_t)v;
         res[2] = len;
     }
 }
@@ -322,13 +309,14 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     if (n == 0) return d_index_used ? hipMemsetAsync(d_index_used, 0, sizeof(uint64_t), s) : hipSuccess;
     const Parts p = parts(d_scratch, n);
     const uint32_t nblk = (n + 255) / 256;
-    decomp_kernel<<<nblk, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
-                                       out_cap, d_out_descs);
-    hipError_t e = hipGetLastError();
+    hipError_t e = hipMemsetAsync(p.counter, 0, 2 * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
-    const uint32_t zl = zstd_lanes(n);
-    zstd_kernel<<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
-                                                 out_cap, d_out_descs, p.zws);
+    decomp_wave_kernel<kFamLz><<<decomp_waves(n), 64, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
+                                                             d_dres, d_out, out_cap, d_out_descs, p.counter, p.lits);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    decomp_wave_kernel<kFamZstd><<<decomp_waves(n), 64, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
+                                                               p.block_sum, d_dres, d_out, out_cap, d_out_descs,
+                                                               p.counter + 1, p.lits);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = launch_plan(d_out_descs, n, d_out, d_index_used, p.vscratch, s)) != hipSuccess) return e;
     if ((e = launch_run(d_out_descs, n, d_out, d_vres2, d_index, index_cap, p.vscratch, d_tables, grid, s, ov)) !=
@@ -344,9 +332,11 @@ hipError_t launch_uncompress_bound(uint32_t codec, const uint8_t* d_in, uint64_t
     return hipGetLastError();
 }
 
+size_t uncompress_scratch_bytes() { return kLitScratch; }
+
 hipError_t launch_uncompress_one(uint32_t codec, const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint64_t cap,
-                                 uint64_t* d_res, hipStream_t s) {
-    uncompress_one_kernel<<<1, 64, 0, s>>>(codec, d_in, n, d_out, cap, d_res);
+                                 uint64_t* d_res, uint8_t* d_lits, hipStream_t s) {
+    uncompress_one_kernel<<<1, 64, 0, s>>>(codec, d_in, n, d_out, cap, d_res, d_lits);
     return hipGetLastError();
 }
 

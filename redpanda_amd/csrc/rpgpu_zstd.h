@@ -57,13 +57,10 @@
 #define RPZ_FAIL(v) (v)
 #endif
 
-// Once-per-block functions are kept out of line on the device: inlined at
-// every call site the kernel's code outgrew the instruction cache.
-#if defined(__HIPCC__) && !defined(RPZ_INLINE_ALL)
-#define RPZ_COLD __host__ __device__ __attribute__((noinline))
-#else
+// Once-per-block functions.  On the device they run inside the wave kernel
+// with the workspace in LDS: inlined, so its accesses stay ds_read / ds_write
+// (through a generic pointer they would become flat accesses).
 #define RPZ_COLD RPC_HD
-#endif
 
 namespace rpzstd {
 
@@ -217,10 +214,10 @@ RPC_HD void copy_seq_match(uint8_t* dst, uint64_t off, uint64_t n) {
     }
     const uint64_t step = off * (16 / off);
     B16 p;
-    p.w[0] = (uint32_t)lo;
-    p.w[1] = (uint32_t)(lo >> 32);
-    p.w[2] = (uint32_t)hi;
-    p.w[3] = (uint32_t)(hi >> 32);
+    p[0] = (uint32_t)lo;
+    p[1] = (uint32_t)(lo >> 32);
+    p[2] = (uint32_t)hi;
+    p[3] = (uint32_t)(hi >> 32);
     uint64_t i = 0;
     for (; i + 16 <= n; i += step) rpcodec::st16(dst + i, p);
     if (i < n) st_part(dst + i, lo, hi, n - i);
@@ -229,7 +226,7 @@ RPC_HD void copy_seq_match(uint8_t* dst, uint64_t off, uint64_t n) {
 RPC_HD void fill_bytes(uint8_t* dst, uint8_t v, uint64_t n) {
     const uint64_t x = 0x0101010101010101ull * v;
     rpcodec::B16 p;
-    p.w[0] = p.w[1] = p.w[2] = p.w[3] = (uint32_t)x;
+    p[0] = p[1] = p[2] = p[3] = (uint32_t)x;
     uint64_t i = 0;
     for (; i + 16 <= n; i += 16) rpcodec::st16(dst + i, p);
     if (i < n) st_part(dst + i, x, x, n - i);
@@ -681,6 +678,56 @@ RPC_HD bool huf_stream(const Ws& w, const uint8_t* src, uint64_t len, uint8_t* o
     return h.ok;
 }
 
+// The four streams of a 4-stream literals section: stream k decodes nsym[k]
+// symbols from s[k] (len[k] bytes) and stores the first nwrite[k] at d[k].
+struct Huf4 {
+    const uint8_t* s[4];
+    uint64_t len[4], nsym[4], nwrite[4];
+    uint8_t* d[4];
+};
+
+// ---------------------------------------------------------------- emitters
+// Everything the decoder decides (acceptance, lengths, offsets, where the
+// literals go) comes from the input alone; the bytes are produced through an
+// emitter.  DirectEmit copies at once, exactly (the host fuzz build and the
+// restatement's reference semantics): Huffman / RLE literals are decoded into
+// the tail of the output slot and read back by the sequences, four streams
+// interleaved one symbol each per step.  The device's wave-cooperative
+// emitter (rpgpu_wave.h) decodes the four streams on four lanes into a
+// scratch buffer and executes sequences 64 at a time with the whole wave.
+struct DirectEmit {
+    RPC_HD void lits(uint8_t* dst, const uint8_t* src, uint64_t n) { copy_lits(dst, src, n); }
+    RPC_HD void match(uint8_t* dst, uint64_t off, uint64_t n) { copy_seq_match(dst, off, n); }
+    RPC_HD void fill(uint8_t* dst, uint8_t v, uint64_t n) { fill_bytes(dst, v, n); }
+    RPC_HD void sync() {}
+    // where a block's Huffman / RLE literals are decoded
+    RPC_HD uint8_t* litbuf(uint8_t* out, uint64_t tail, uint64_t size) { return out + tail - size; }
+    RPC_HD void litfill(uint8_t* d, uint8_t v, uint64_t n) { fill_bytes(d, v, n); }
+    RPC_HD bool huf1(const Ws& w, const uint8_t* src, uint64_t len, uint8_t* d, uint64_t n) {
+        return huf_stream(w, src, len, d, n, n);
+    }
+    RPC_HD bool huf4(const Ws& w, const Huf4& a) {
+        const uint32_t L = w.huf_log;
+        const bool x2 = w.huf_x2 != 0;
+        HufS h0, h1, h2, h3;
+        huf_begin(h0, a.s[0], a.len[0], a.d[0], a.nsym[0], a.nwrite[0]);
+        huf_begin(h1, a.s[1], a.len[1], a.d[1], a.nsym[1], a.nwrite[1]);
+        huf_begin(h2, a.s[2], a.len[2], a.d[2], a.nsym[2], a.nwrite[2]);
+        huf_begin(h3, a.s[3], a.len[3], a.d[3], a.nsym[3], a.nwrite[3]);
+        if (!h0.live) huf_end(h0);
+        if (!h1.live) huf_end(h1);
+        if (!h2.live) huf_end(h2);
+        if (!h3.live) huf_end(h3);
+        while (h0.live | h1.live | h2.live | h3.live) {
+            huf_step(w, h0, L, x2);
+            huf_step(w, h1, L, x2);
+            huf_step(w, h2, L, x2);
+            huf_step(w, h3, L, x2);
+        }
+        return h0.ok && h1.ok && h2.ok && h3.ok;
+    }
+};
+
 // ---------------------------------------------------------------- blocks
 struct Lit {
     const uint8_t* p;  // literal bytes (input, or the output slot's tail)
@@ -689,7 +736,9 @@ struct Lit {
 
 // ZSTD_decodeLiteralsBlock.  Huffman / RLE literals go to out[tail - n, tail).
 // Returns section bytes, -1 on error, -2 when the tail would reach `op`.
-RPZ_COLD int64_t literals(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t op, uint64_t tail, Lit& lit) {
+template <class E>
+RPZ_COLD int64_t literals(E& em, Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t op, uint64_t tail,
+                          Lit& lit) {
     if (n < 3) return RPZ_FAIL(-1);  // MIN_CBLOCK_SIZE
     const uint32_t type = in[0] & 3, lh = (in[0] >> 2) & 3;
     if (type == 0 || type == 1) {  // raw / RLE
@@ -713,9 +762,9 @@ RPZ_COLD int64_t literals(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, ui
         if (lh == 3 && n < 4) return RPZ_FAIL(-1);
         if (size > kBlockMax) return RPZ_FAIL(-1);
         if (size > tail - op) return -2;
-        uint8_t* d = out + tail - size;
+        uint8_t* d = em.litbuf(out, tail, size);
         const uint8_t v = in[hs];
-        fill_bytes(d, v, size);
+        em.litfill(d, v, size);
         lit.p = d;
         lit.n = size;
         return (int64_t)(hs + 1);
@@ -757,9 +806,9 @@ RPZ_COLD int64_t literals(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, ui
         slen -= (uint64_t)th;
     }
     if (size > tail - op) return -2;
-    uint8_t* d = out + tail - size;
+    uint8_t* d = em.litbuf(out, tail, size);
     if (single) {
-        if (!huf_stream(w, src, slen, d, size, size)) return RPZ_FAIL(-1);
+        if (!em.huf1(w, src, slen, d, size)) return RPZ_FAIL(-1);
     } else {
         if (slen < 10) return RPZ_FAIL(-1);
         const uint64_t l1 = le16(src), l2 = le16(src + 2), l3 = le16(src + 4);
@@ -773,33 +822,26 @@ RPZ_COLD int64_t literals(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, ui
                 !bits_init(t, src + 6 + l1 + l2, l3) || !bits_init(t, src + 6 + l1 + l2 + l3, l4))
                 return RPZ_FAIL(-1);
         }
-        // the four streams, interleaved one symbol each per step
-        const uint32_t L = w.huf_log;
-        const bool x2 = w.huf_x2 != 0;
-        HufS h0, h1, h2, h3;
-        const uint64_t n3 = size > 3 * seg ? size - 3 * seg : 0;
         // stream k: symbols [k*seg, ...), writes clipped to the section size
+        const uint64_t n3 = size > 3 * seg ? size - 3 * seg : 0;
         const uint64_t at1 = seg, at2 = 2 * seg, at3 = 3 * seg;
-        const uint64_t w0 = size < seg ? size : seg;
-        const uint64_t w1 = at1 >= size ? 0 : (size - at1 < seg ? size - at1 : seg);
-        const uint64_t w2 = at2 >= size ? 0 : (size - at2 < seg ? size - at2 : seg);
-        const uint64_t w3 = at3 >= size ? 0 : (size - at3 < n3 ? size - at3 : n3);
-        const uint8_t* s0 = src + 6;
-        huf_begin(h0, s0, l1, d, seg, w0);
-        huf_begin(h1, s0 + l1, l2, d + (at1 < size ? at1 : 0), seg, w1);
-        huf_begin(h2, s0 + l1 + l2, l3, d + (at2 < size ? at2 : 0), seg, w2);
-        huf_begin(h3, s0 + l1 + l2 + l3, l4, d + (at3 < size ? at3 : 0), n3, w3);
-        if (!h0.live) huf_end(h0);
-        if (!h1.live) huf_end(h1);
-        if (!h2.live) huf_end(h2);
-        if (!h3.live) huf_end(h3);
-        while (h0.live | h1.live | h2.live | h3.live) {
-            huf_step(w, h0, L, x2);
-            huf_step(w, h1, L, x2);
-            huf_step(w, h2, L, x2);
-            huf_step(w, h3, L, x2);
-        }
-        if (!(h0.ok && h1.ok && h2.ok && h3.ok)) return RPZ_FAIL(-1);
+        Huf4 a;
+        a.s[0] = src + 6;
+        a.s[1] = a.s[0] + l1;
+        a.s[2] = a.s[1] + l2;
+        a.s[3] = a.s[2] + l3;
+        a.len[0] = l1, a.len[1] = l2, a.len[2] = l3, a.len[3] = l4;
+        a.nsym[0] = a.nsym[1] = a.nsym[2] = seg;
+        a.nsym[3] = n3;
+        a.nwrite[0] = size < seg ? size : seg;
+        a.nwrite[1] = at1 >= size ? 0 : (size - at1 < seg ? size - at1 : seg);
+        a.nwrite[2] = at2 >= size ? 0 : (size - at2 < seg ? size - at2 : seg);
+        a.nwrite[3] = at3 >= size ? 0 : (size - at3 < n3 ? size - at3 : n3);
+        a.d[0] = d;
+        a.d[1] = d + (at1 < size ? at1 : 0);
+        a.d[2] = d + (at2 < size ? at2 : 0);
+        a.d[3] = d + (at3 < size ? at3 : 0);
+        if (!em.huf4(w, a)) return RPZ_FAIL(-1);
     }
     w.lit_entropy = 1;
     lit.p = d;
@@ -865,14 +907,15 @@ RPC_HD int64_t seq_table_impl(Ws& w, uint32_t mode, uint32_t which, const uint8_
 // ZSTD_decompressBlock_internal for one compressed block: output at out[op..),
 // history from out[fstart..), at most `cap` bytes; literals may use the slot
 // tail [.., tail).  Returns bytes produced, -1 error, -2 slot exceeded.
-RPZ_COLD int64_t block(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t fstart, uint64_t op, uint64_t cap,
-                     uint64_t tail) {
+template <class E>
+RPZ_COLD int64_t block(E& em, Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t fstart, uint64_t op,
+                       uint64_t cap, uint64_t tail) {
     if (n >= kBlockMax) return RPZ_FAIL(-1);
     Lit lit;
 #if RPZ_PROF
     const uint64_t c0 = RPZ_CLK();
 #endif
-    const int64_t lh = literals(w, in, n, out, op, tail, lit);
+    const int64_t lh = literals(em, w, in, n, out, op, tail, lit);
     if (lh < 0) return lh;
 #if RPZ_PROF
     const uint64_t c1 = RPZ_CLK();
@@ -967,9 +1010,9 @@ RPZ_COLD int64_t block(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint6
             if (ll > (uint64_t)(lend - lp)) return RPZ_FAIL(-1);
             const uint64_t lit_end = o + ll;
             if (offset > lit_end - fstart) return RPZ_FAIL(-1);
-            copy_lits(out + o, lp, ll);
+            em.lits(out + o, lp, ll);
             lp += ll;
-            copy_seq_match(out + lit_end, offset, ml);
+            em.match(out + lit_end, offset, ml);
             o = lit_end + ml;
         }
 #if RPZ_PROF
@@ -983,7 +1026,7 @@ RPZ_COLD int64_t block(Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint6
     }
     const uint64_t last = (uint64_t)(lend - lp);
     if (last > oend - o) return RPZ_FAIL(-1);
-    copy_lits(out + o, lp, last);
+    em.lits(out + o, lp, last);
     o += last;
     return (int64_t)(o - op);
 }
@@ -1130,7 +1173,9 @@ RPC_HD bool adapt(Bufs& s, uint64_t need_in, uint64_t need_out) {
 // One call of the wrapper over one buffer.  out[0, cap) is the output slot.
 // Returns a verdict; *out_len = bytes produced.  `cap` too small for what the
 // library would produce -> V_OVERFLOW.
-RPC_HD int32_t uncompress_impl(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len, Ws& w) {
+template <class E>
+RPC_HD int32_t uncompress_impl(E& em, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len,
+                               Ws& w) {
     uint64_t T = 0, p = 0;
     uint64_t S = 0;  // fill of the 64 KiB staging buffer `out` (may sit full)
     Bufs bufs{0, 0, 0};
@@ -1179,20 +1224,20 @@ RPC_HD int32_t uncompress_impl(const uint8_t* in, uint64_t n, uint8_t* out, uint
                 if (type == 2) {
                     if (T > cap) return V_OVERFLOW;
                     const uint64_t lim = fend < cap ? fend : cap;
-                    r = block(w, f + ip, size, out, fstart, T, lim - T, cap);
+                    r = block(em, w, f + ip, size, out, fstart, T, lim - T, cap);
                     if (r == -2 || (r < 0 && lim < fend)) return fend <= cap ? V_ERROR : V_OVERFLOW;
                     if (r < 0) return RPZ_FAIL(V_ERROR);
                     ip += size;
                 } else if (type == 0) {
                     if (size > fend - T) return RPZ_FAIL(V_ERROR);
                     if (T + size > cap) return V_OVERFLOW;
-                    copy_lits(out + T, f + ip, size);
+                    em.lits(out + T, f + ip, size);
                     r = (int64_t)size;
                     ip += size;
                 } else {
                     if (size > fend - T) return RPZ_FAIL(V_ERROR);
                     if (T + size > cap) return V_OVERFLOW;
-                    fill_bytes(out + T, f[ip], size);
+                    em.fill(out + T, f[ip], size);
                     r = (int64_t)size;
                     ip += 1;
                 }
@@ -1201,6 +1246,7 @@ RPC_HD int32_t uncompress_impl(const uint8_t* in, uint64_t n, uint8_t* out, uint
             }
             if (T != fend) return RPZ_FAIL(V_ERROR);
             if (h.csum) {
+                em.sync();  // the checksum reads the decoded bytes
                 if ((uint32_t)xxh64(out + fstart, T - fstart) != le32(f + ip)) return RPZ_FAIL(V_ERROR);
             }
             S += h.fcs;  // decoded straight into the staging buffer
@@ -1237,7 +1283,7 @@ RPC_HD int32_t uncompress_impl(const uint8_t* in, uint64_t n, uint8_t* out, uint
                     if (take == 0) break;
                     if (take > room_ring) return RPZ_FAIL(V_ERROR);
                     if (T + take > cap) return V_OVERFLOW;
-                    copy_lits(out + T, f + ip, take);
+                    em.lits(out + T, f + ip, take);
                     ip += take;
                     T += take;
                     decoded += take;
@@ -1249,7 +1295,7 @@ RPC_HD int32_t uncompress_impl(const uint8_t* in, uint64_t n, uint8_t* out, uint
                     if (size > room_ring) return RPZ_FAIL(V_ERROR);
                     if (size > h.bsm) return RPZ_FAIL(V_ERROR);
                     if (T + size > cap) return V_OVERFLOW;
-                    fill_bytes(out + T, f[ip], size);
+                    em.fill(out + T, f[ip], size);
                     ip += 1;
                     r = size;
                     T += r;
@@ -1259,7 +1305,7 @@ RPC_HD int32_t uncompress_impl(const uint8_t* in, uint64_t n, uint8_t* out, uint
                     if (avail < size) break;  // waits in the load stage
                     if (T > cap) return V_OVERFLOW;
                     const uint64_t lim = room_ring < cap - T ? room_ring : cap - T;
-                    const int64_t rr = block(w, f + ip, size, out, fstart, T, lim, cap);
+                    const int64_t rr = block(em, w, f + ip, size, out, fstart, T, lim, cap);
                     if (rr == -2 || (rr < 0 && lim < room_ring)) {
                         // the slot, not the library, ran out: decide with the bound
                         return V_OVERFLOW;
@@ -1293,6 +1339,7 @@ RPC_HD int32_t uncompress_impl(const uint8_t* in, uint64_t n, uint8_t* out, uint
                 if (cb != 0 && h.fcs != kUnknown && decoded != h.fcs) return RPZ_FAIL(V_ERROR);
                 if (h.csum) {
                     if (rem - ip < 4) break;
+                    em.sync();
                     if ((uint32_t)xxh64(out + fstart, T - fstart) != le32(f + ip)) return RPZ_FAIL(V_ERROR);
                     ip += 4;
                 }
@@ -1368,10 +1415,12 @@ RPC_HD uint64_t bound(const uint8_t* in, uint64_t n) {
     return b;
 }
 
-RPC_HD int32_t uncompress(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len, Ws& w) {
+template <class E>
+RPC_HD int32_t uncompress(E& em, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len, Ws& w) {
     *out_len = 0;
     if (n == 0) return RPZ_FAIL(V_ERROR);  // "Asked to stream_zstd::uncompress empty buffer"
-    const int32_t v = uncompress_impl(in, n, out, cap, out_len, w);
+    const int32_t v = uncompress_impl(em, in, n, out, cap, out_len, w);
+    em.sync();
     if (v == V_OVERFLOW && bound(in, n) <= cap) return RPZ_FAIL(V_ERROR);
     return v;
 }

@@ -337,7 +337,8 @@ void check(int codec, const Bytes& in, const char* what, long id) {
     const uint64_t bound = rpcodec::uncompress_bound((uint32_t)codec, ib.data(), n);
     Bytes ob(bound + rpcodec::kSlack + (g_exact ? 0 : 64), 0x5A);
     uint64_t glen = 0;
-    const int32_t gv = rpcodec::uncompress((uint32_t)codec, ib.data(), n, ob.data(), bound, &glen);
+    rpcodec::DirectEmit em;
+    const int32_t gv = rpcodec::uncompress(em, (uint32_t)codec, ib.data(), n, ob.data(), bound, &glen);
     const size_t ocap = bound + (1u << 20);
     Bytes rb(ocap);
     size_t rlen = 0;

@@ -286,7 +286,8 @@ void compare(const Bytes& in) {
     Bytes eout(g_exact ? cap + rpcodec::kSlack : cap + 1);
     static rpzstd::Ws ws;
     uint64_t elen = 0;
-    const int32_t ev = rpzstd::uncompress(ip, in.size(), eout.data(), cap, &elen, ws);
+    rpzstd::DirectEmit em;
+    const int32_t ev = rpzstd::uncompress(em, ip, in.size(), eout.data(), cap, &elen, ws);
     static Bytes oout(96u << 20);
     size_t olen = 0;
     const int32_t ov = orc_uncompress(4, ip, in.size(), oout.data(), oout.size(), &olen);

@@ -238,3 +238,14 @@ def eng_default_uncompress(frame):
 
     with engine.Engine(0) as e:
         return e.uncompress(4, frame, cap=16 << 20)
+
+
+@pytest.mark.parametrize("codec", [2, 3, 4])
+def test_mutated_payloads_many(eng, codec):
+    """Differential fuzz of the wave-cooperative device decoders (rpgpu_wave.h)
+    against the oracle: 600 library frames per codec, most of them mutated
+    (truncation, flipped bytes, junk, second frames, 0xFF bytes), in one arena."""
+    rng = np.random.default_rng(900 + codec)
+    bs = [batch(c, fmt=WIRE, record_count=rc, attrs=codec) for c, rc in mutated_bodies(rng, codec, 600)]
+    data, descs = arena(bs, fmt=WIRE, ops=OPS)
+    compare(eng.decompress_arena(data, descs), data, descs)
