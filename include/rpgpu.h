@@ -97,6 +97,11 @@ enum rpgpu_verdict {
     /* multi-batch record sets (kafka/protocol/batch_reader.cc:50-58) */
     RPGPU_V_SET_HEADER_SHORT = 36, /* < 61 bytes left for the next batch header:
                                       corrupt_message "Invalid kafka header parsing" */
+    /* stream parser (storage/parser.cc:223-299, parser_errc) */
+    RPGPU_V_END_OF_STREAM = 23,    /* parser_errc::end_of_stream (benign)         */
+    RPGPU_V_READ_OFFSET_REGRESSION = 24, /* skipping_consumer throws: batch base
+                                      offset below the expected next one
+                                      (storage/log_reader.cc:30-38)             */
     /* segment index (storage/index_state.cc:48-54) */
     RPGPU_V_INDEX_OFFSET_BELOW_BASE = 37, /* vassert: batch base offset below the segment's */
     RPGPU_V_SKIPPED = 40,          /* not decompressed: no RPGPU_OP_DECOMP, not
@@ -427,6 +432,81 @@ int32_t rpgpu_segment_index_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_des
                                    const rpgpu_batch_result* d_results, const rpgpu_segment* d_segs,
                                    uint32_t nsegs, rpgpu_segment_state* d_states,
                                    rpgpu_index_entry* d_entries, void* hip_stream);
+
+/* ---- stream-level storage parser -------------------------------------------
+ * Replaces storage::continuous_batch_parser::consume (storage/parser.cc:
+ * 113-299) over one segment file region per rpgpu_segment_read, driving one of
+ * the reference's consumers (storage/parser.h:33-91):
+ *   RPGPU_PARSE_RECOVERY  log_replayer's checksumming_consumer
+ *                         (storage/log_replayer.cc:26-92): every batch whose
+ *                         header parses is accepted; its body CRC and the stop
+ *                         at the first bad one are left to rpgpu_run_device +
+ *                         rpgpu_segment_index_device over the emitted batches;
+ *   RPGPU_PARSE_READER    log_segment_batch_reader's skipping_consumer
+ *                         (storage/log_reader.cc:28-121): accept / skip / stop
+ *                         by offset range, batch type, timestamp, byte budget,
+ *                         stable offset, next cached batch and the 32 KiB
+ *                         reader buffer, as one read_some call does
+ *                         (log_reader.cc:164-215).
+ * The parser follows the size_bytes chain: per batch it reads the 61-byte
+ * little-endian header (an empty read ends the stream, a short one is
+ * input_stream_not_enough_bytes, all zeros is a fallocated tail), checks the
+ * header CRC, asks the consumer, then reads (accept) or skips the body; the
+ * result is the bytes consumed, or the error when nothing was consumed.
+ * Each accepted batch becomes an on-disk rpgpu_batch_desc at
+ * d_descs[desc_first + k] (k < desc_cap) for rpgpu_run_device. */
+enum rpgpu_parse_mode {
+    RPGPU_PARSE_RECOVERY = 0,
+    RPGPU_PARSE_READER = 1,
+};
+
+typedef struct rpgpu_segment_read {
+    uint64_t offset;          /* the segment's bytes in the arena             */
+    uint64_t length;          /* bytes the input stream yields                */
+    uint32_t desc_first;      /* first output descriptor slot                 */
+    uint32_t desc_cap;        /* slots available                              */
+    uint32_t partition;       /* copied into the emitted descriptors          */
+    uint8_t mode;             /* enum rpgpu_parse_mode                        */
+    uint8_t ops;              /* rpgpu_op mask of the emitted descriptors     */
+    uint8_t has_type_filter;  /* log_reader_config::type_filter set           */
+    int8_t type_filter;
+    /* log_reader_config (storage/types.h:270-300), READER mode */
+    uint8_t has_first_timestamp;
+    uint8_t strict_max_bytes;
+    uint8_t has_next_cached;  /* skipping_consumer::_next_cached_batch set    */
+    uint8_t reserved0;
+    uint32_t reserved1;
+    int64_t start_offset, max_offset, first_timestamp;
+    int64_t stable_offset;    /* segment offsets().stable_offset              */
+    int64_t next_cached_batch;
+    int64_t expected_next_batch; /* skipping_consumer::_expected_next_batch
+                                    (model::offset{} = INT64_MIN)             */
+    uint64_t max_bytes, bytes_consumed;
+    uint64_t max_buffer;      /* reader buffer limit; 0 = 32 KiB (log_reader.h:91) */
+} rpgpu_segment_read;         /* 112 bytes */
+
+typedef struct rpgpu_segment_parse_result {
+    int32_t status;        /* RPGPU_OK when consume() returned a byte count;
+                              else the parser_errc verdict, or
+                              RPGPU_V_READ_OFFSET_REGRESSION (an exception)     */
+    int32_t last_error;    /* the parser's _err: OK, END_OF_STREAM,
+                              FALLOCATED_ZERO, STREAM_SHORT, HDR_CRC_MISMATCH   */
+    uint32_t accepted;     /* batches accepted (descriptors emitted, up to cap) */
+    uint32_t skipped;      /* batches skipped                                  */
+    uint64_t bytes_consumed;   /* the parser's _bytes_consumed                  */
+    uint64_t physical_offset;  /* _physical_base_offset when the parser stopped */
+    int64_t start_offset;      /* READER: log_reader_config::start_offset after */
+    uint64_t cfg_bytes_consumed; /* READER: log_reader_config::bytes_consumed   */
+    int64_t expected_next_batch; /* READER: skipping_consumer state after      */
+    uint8_t over_budget;       /* READER: log_reader_config::over_budget        */
+    uint8_t stopped;           /* the consumer stopped the parser               */
+    uint16_t reserved0;
+    uint32_t reserved1;
+} rpgpu_segment_parse_result;  /* 64 bytes */
+
+int32_t rpgpu_segment_parse_device(rpgpu_ctx* ctx, const uint8_t* d_data, const rpgpu_segment_read* d_reads,
+                                   uint32_t nreads, rpgpu_segment_parse_result* d_results,
+                                   rpgpu_batch_desc* d_descs, void* hip_stream);
 
 /* ---- partition summaries (multi-GPU gather) -------------------------------
  * Per partition p of [part_lo, part_lo + nparts), over the batches of

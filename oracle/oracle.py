@@ -85,6 +85,8 @@ def lib() -> C.CDLL:
         L.orc_record_sets_split.restype = u64
         L.orc_record_sets_split.argtypes = [vp, u32, vp, vp, u64, vp, vp, vp]
         L.orc_record_sets_reduce.restype = None
+        L.orc_segment_parse.restype = None
+        L.orc_segment_parse.argtypes = [vp, vp, vp, vp]
         L.orc_segment_index.restype = None
         L.orc_segment_index.argtypes = [vp, vp, vp, u32, vp, vp]
         L.orc_record_sets_reduce.argtypes = [u32, vp, vp, vp, vp, vp]
@@ -236,3 +238,19 @@ def segment_index(descs: np.ndarray, results: np.ndarray, segs: np.ndarray):
     lib().orc_segment_index(descs.ctypes.data, results.ctypes.data, segs.ctypes.data, len(segs),
                             states.ctypes.data, entries.ctypes.data)
     return states, entries[:len(descs)]
+
+
+def segment_parse(data: np.ndarray, reads: np.ndarray):
+    """continuous_batch_parser::consume per segment read (oracle/parse.c):
+    (results, descs) with descriptor slots laid out as the reads ask."""
+    from redpanda_amd.abi import SEGMENT_PARSE_RESULT_DTYPE, SEGMENT_READ_DTYPE
+
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    reads = np.ascontiguousarray(reads, dtype=SEGMENT_READ_DTYPE)
+    res = np.zeros(len(reads), dtype=SEGMENT_PARSE_RESULT_DTYPE)
+    ncap = int((reads["desc_first"].astype(np.int64) + reads["desc_cap"]).max()) if len(reads) else 0
+    descs = np.zeros(max(ncap, 1), dtype=DESC_DTYPE)
+    for i in range(len(reads)):
+        lib().orc_segment_parse(data.ctypes.data, reads[i:i + 1].ctypes.data, res[i:i + 1].ctypes.data,
+                                descs.ctypes.data)
+    return res, descs[:ncap]

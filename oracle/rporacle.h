@@ -107,6 +107,11 @@ void orc_segment_index(const rpgpu_batch_desc* descs, const rpgpu_batch_result* 
                        const rpgpu_segment* segs, uint32_t nsegs, rpgpu_segment_state* states,
                        rpgpu_index_entry* entries);
 
+/* storage::continuous_batch_parser::consume (storage/parser.cc:113-299) with
+ * the checksumming / skipping consumers (oracle/parse.c) */
+void orc_segment_parse(const uint8_t* data, const rpgpu_segment_read* rd, rpgpu_segment_parse_result* out,
+                       rpgpu_batch_desc* descs);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,6 +40,8 @@ V_REC_UNDEFINED = 11
 V_HDR_CRC_MISMATCH = 20
 V_STREAM_SHORT = 21
 V_FALLOCATED_ZERO = 22
+V_END_OF_STREAM = 23
+V_READ_OFFSET_REGRESSION = 24
 V_DECOMP_ERROR = 30
 V_LZ4_TRAILING = 32
 V_DECOMP_UNSUPPORTED = 33
@@ -95,6 +97,22 @@ SEGMENT_STATE_DTYPE = np.dtype([("status", "<i4"), ("entries", "<u4"), ("tracked
                                 ("monotonic", "u1"), ("non_data_timestamps", "u1"), ("reserved", "<u2"),
                                 ("max_offset", "<i8"), ("base_timestamp", "<i8"), ("max_timestamp", "<i8"),
                                 ("acc", "<u8")])
+PARSE_RECOVERY = 0
+PARSE_READER = 1
+SEGMENT_READ_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u8"), ("desc_first", "<u4"), ("desc_cap", "<u4"),
+                               ("partition", "<u4"), ("mode", "u1"), ("ops", "u1"), ("has_type_filter", "u1"),
+                               ("type_filter", "i1"), ("has_first_timestamp", "u1"), ("strict_max_bytes", "u1"),
+                               ("has_next_cached", "u1"), ("reserved0", "u1"), ("reserved1", "<u4"),
+                               ("start_offset", "<i8"), ("max_offset", "<i8"), ("first_timestamp", "<i8"),
+                               ("stable_offset", "<i8"), ("next_cached_batch", "<i8"),
+                               ("expected_next_batch", "<i8"), ("max_bytes", "<u8"), ("bytes_consumed", "<u8"),
+                               ("max_buffer", "<u8")])
+SEGMENT_PARSE_RESULT_DTYPE = np.dtype([("status", "<i4"), ("last_error", "<i4"), ("accepted", "<u4"),
+                                       ("skipped", "<u4"), ("bytes_consumed", "<u8"), ("physical_offset", "<u8"),
+                                       ("start_offset", "<i8"), ("cfg_bytes_consumed", "<u8"),
+                                       ("expected_next_batch", "<i8"), ("over_budget", "u1"), ("stopped", "u1"),
+                                       ("reserved0", "<u2"), ("reserved1", "<u4")])
+assert SEGMENT_READ_DTYPE.itemsize == 112 and SEGMENT_PARSE_RESULT_DTYPE.itemsize == 64
 INDEX_ENTRY_DTYPE = np.dtype([("relative_offset", "<u4"), ("relative_time", "<u4"), ("position", "<u8")])
 assert SEGMENT_DTYPE.itemsize == 32 and SEGMENT_STATE_DTYPE.itemsize == 48 and INDEX_ENTRY_DTYPE.itemsize == 16
 assert INDEX_DTYPE.itemsize == 32 and RP_HEADER_DTYPE.itemsize == 61
@@ -184,6 +202,7 @@ def lib() -> C.CDLL:
         _sig(L.rpgpu_eventfd, C.c_int, _vp)
         _sig(L.rpgpu_kafka_error_code, _i32, _vp, _u32)
         _sig(L.rpgpu_kafka_error_codes_device, _i32, _vp, _vp, _u32, _u32, _vp, _vp)
+        _sig(L.rpgpu_segment_parse_device, _i32, _vp, _vp, _vp, _u32, _vp, _vp, _vp)
         _sig(L.rpgpu_partition_summaries_device, _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
         if not hasattr(L, "rpgpu_decomp_scratch_bytes"):  # an older build (A/B timing runs)
             _LIB = L
@@ -222,7 +241,7 @@ EXPORTED = [
     "rpgpu_abi_version", "rpgpu_open", "rpgpu_close", "rpgpu_last_error", "rpgpu_device_info",
     "rpgpu_arena_alloc", "rpgpu_arena_free", "rpgpu_submit", "rpgpu_poll", "rpgpu_wait",
     "rpgpu_eventfd", "rpgpu_kafka_error_code", "rpgpu_kafka_error_codes_device",
-    "rpgpu_partition_summaries_device",
+    "rpgpu_partition_summaries_device", "rpgpu_segment_parse_device",
     "rpgpu_validate_scratch_bytes", "rpgpu_validate_device", "rpgpu_plan_device",
     "rpgpu_run_device", "rpgpu_crc32c_ranges_device",
     "rpgpu_crc32c_extend", "rpgpu_internal_header_only_crc", "rpgpu_crc_record_batch",

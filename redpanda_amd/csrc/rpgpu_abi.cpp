@@ -64,6 +64,9 @@ hipError_t launch_uncompress_one(uint32_t codec, const uint8_t* d_in, uint64_t n
 size_t uncompress_scratch_bytes();
 hipError_t launch_kafka_codes(const rpgpu_batch_result* d_res, uint32_t n, uint32_t batch_max_bytes,
                               int32_t* d_codes, hipStream_t s);
+hipError_t launch_segment_parse(const uint8_t* d_data, const rpgpu_segment_read* d_reads, uint32_t n,
+                                rpgpu_segment_parse_result* d_res, rpgpu_batch_desc* d_descs,
+                                const uint32_t* d_tables, int grid, hipStream_t s);
 hipError_t launch_summaries(const rpgpu_batch_desc* d_descs, const rpgpu_batch_result* d_res, uint32_t n,
                             uint32_t part_lo, uint32_t nparts, int64_t* d_out, hipStream_t s);
 }  // namespace rpgpu
@@ -234,6 +237,16 @@ int rpgpu_eventfd(rpgpu_ctx* c) { return c ? c->efd : -1; }
 int32_t rpgpu_kafka_error_code(const rpgpu_batch_result* r, uint32_t batch_max_bytes) {
     if (!r) return RPGPU_KAFKA_ERR_UNKNOWN_SERVER_ERROR;
     return rpgpu::kafka_error_code(r->verdict, r->size_bytes, batch_max_bytes);
+}
+
+int32_t rpgpu_segment_parse_device(rpgpu_ctx* c, const uint8_t* d_data, const rpgpu_segment_read* d_reads,
+                                   uint32_t nreads, rpgpu_segment_parse_result* d_results,
+                                   rpgpu_batch_desc* d_descs, void* hip_stream) {
+    if (!c || (nreads && (!d_data || !d_reads || !d_results || !d_descs))) return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_segment_parse(d_data, d_reads, nreads, d_results, d_descs, c->d_tables, c->grid, s);
+    if (e != hipSuccess) return fail(c, e, "segment parse launch");
+    return RPGPU_OK;
 }
 
 int32_t rpgpu_partition_summaries_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs,

@@ -695,6 +695,182 @@ __global__ __launch_bounds__(kValidateThreads) void crc_ranges_kernel(
     }
 }
 
+// ------------------------------------------------ stream-level storage parser
+// storage::continuous_batch_parser::consume (storage/parser.cc:113-299) over
+// one segment region per wavefront, with log_replayer's checksumming consumer
+// (accept all) or log_reader's skipping_consumer (storage/log_reader.cc:
+// 28-121).  The walk follows the size_bytes chain, so it is serial per
+// segment: each step is one 64-byte header load (16 lanes x 4 B), the header
+// CRC on all 64 lanes (header_crc_vec) and a wave-uniform decision.  Many
+// segments (partitions) run side by side; the bodies are not read here --
+// rpgpu_run_device checks them over the emitted descriptors.
+__device__ __forceinline__ bool header_all_zero(const Img64& H) {
+    uint32_t any = 0;
+#pragma unroll
+    for (int i = 0; i < 15; i++) any |= H.w[i];
+    any |= H.w[15] & 0xffu;  // byte 60 only
+    return any == 0;
+}
+
+__global__ __launch_bounds__(kValidateThreads) void segment_parse_kernel(
+    const uint8_t* __restrict__ data, const rpgpu_segment_read* __restrict__ reads, uint32_t nreads,
+    rpgpu_segment_parse_result* __restrict__ results, rpgpu_batch_desc* __restrict__ descs,
+    const uint32_t* __restrict__ tables) {
+    __shared__ __attribute__((aligned(16))) uint32_t sT[kTableWords];
+    load_tables(sT, tables);
+    const uint32_t l = lane_id();
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    for (uint32_t s = gw; s < nreads; s += nw) {
+        const rpgpu_segment_read rd = reads[s];
+        const uint8_t* seg = data + rd.offset;
+        const uint64_t len = rd.length;
+        const bool reader = rd.mode == RPGPU_PARSE_READER;
+        const uint64_t max_buffer = rd.max_buffer ? rd.max_buffer : 32u * 1024u;
+        uint64_t pos = 0, bytes_consumed = 0, phys = 0, buffer = 0;
+        int32_t err = RPGPU_V_OK;
+        bool exception = false, stopped = false, over_budget = false;
+        uint32_t accepted = 0, skipped = 0;
+        int64_t start_offset = rd.start_offset, expected = rd.expected_next_batch;
+        uint64_t cfg_bytes = rd.bytes_consumed;
+        const __amdgpu_buffer_rsrc_t rs = batch_rsrc(seg);
+        for (;;) {
+            const uint64_t rem = len - pos;
+            if (rem == 0) {
+                err = RPGPU_V_END_OF_STREAM;
+                break;
+            }
+            if (rem < (uint64_t)kHeaderSize) {
+                err = RPGPU_V_STREAM_SHORT;
+                break;
+            }
+            // the 64-byte header window at pos (segments are < 2 GiB apart
+            // from their base; the arena's tail pad covers the 3 bytes past 61)
+            const uint32_t hv = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int32_t)(pos + 4 * (l & 15)), 0, 0);
+            Img64 H;
+#pragma unroll
+            for (int i = 0; i < 16; i++) H.w[i] = rdl(hv, i);
+            if (header_all_zero(H)) {
+                err = RPGPU_V_FALLOCATED_ZERO;
+                break;
+            }
+            Img64 D;
+#pragma unroll
+            for (int i = 0; i < 16; i++) D.w[i] = H.w[i];
+            D.w[15] &= 0xffu;
+            if (header_crc_vec(sT, D) != H.w[0]) {
+                err = RPGPU_V_HDR_CRC_MISMATCH;
+                break;
+            }
+            const int32_t size_bytes = (int32_t)H.get_le(4, 4);
+            const int64_t base_offset = (int64_t)H.get_le(8, 8);
+            const int8_t type = (int8_t)H.byte(16);
+            const int32_t lod = (int32_t)H.get_le(23, 4);
+            const int64_t max_ts = (int64_t)H.get_le(35, 8);
+            const int64_t last = base_offset + lod;
+            const uint64_t sz = (uint64_t)(int64_t)size_bytes;
+            int decision = 0;  // 0 accept, 1 skip, 2 stop
+            if (reader) {
+                if (base_offset < expected) {
+                    exception = true;
+                    break;
+                }
+                if (base_offset > rd.max_offset) {
+                    decision = 2;
+                } else if ((rd.strict_max_bytes || cfg_bytes) && cfg_bytes + sz > rd.max_bytes) {
+                    over_budget = true;
+                    decision = 2;
+                } else if (last < start_offset) {
+                    decision = 1;
+                } else if (rd.has_type_filter && rd.type_filter != type) {
+                    start_offset = last + 1;
+                    decision = 1;
+                } else if (rd.has_first_timestamp && rd.first_timestamp > max_ts) {
+                    start_offset = last + 1;
+                    decision = 1;
+                }
+            }
+            if (decision == 2) {
+                stopped = true;
+                break;
+            }
+            const uint64_t body = (uint64_t)((int64_t)size_bytes - kHeaderSize);
+            const uint64_t avail = len - pos - kHeaderSize;
+            if (decision == 1) {
+                expected = last + 1;
+                phys += sz;
+                if (body > avail) {
+                    err = RPGPU_V_STREAM_SHORT;
+                    break;
+                }
+                pos += kHeaderSize + body;
+                bytes_consumed += sz;
+                skipped++;
+                continue;
+            }
+            if (reader) expected = last + 1;
+            phys += sz;
+            if (accepted < rd.desc_cap && l == 0) {
+                rpgpu_batch_desc d;
+                d.offset = rd.offset + pos;
+                d.length = (uint32_t)(body > avail ? avail + kHeaderSize : body + kHeaderSize);
+                d.partition = rd.partition;
+                d.format = RPGPU_FMT_RP_DISK;
+                d.ops = rd.ops;
+                d.flags = 0;
+                d.reserved = 0;
+                descs[rd.desc_first + accepted] = d;
+            }
+            accepted++;
+            bytes_consumed += sz;
+            if (body > avail) {
+                err = RPGPU_V_STREAM_SHORT;
+                break;
+            }
+            pos += kHeaderSize + body;
+            if (reader) {
+                start_offset = last + 1;
+                cfg_bytes += sz;
+                buffer += sz;
+                if (last >= rd.stable_offset || last >= rd.max_offset ||
+                    (rd.has_next_cached && rd.next_cached_batch == last + 1) || cfg_bytes >= rd.max_bytes ||
+                    buffer >= max_buffer) {
+                    stopped = true;
+                    break;
+                }
+            }
+        }
+        if (l == 0) {
+            rpgpu_segment_parse_result r;
+            r.last_error = exception ? RPGPU_V_OK : err;
+            const bool benign = err == RPGPU_V_OK || err == RPGPU_V_END_OF_STREAM || err == RPGPU_V_FALLOCATED_ZERO;
+            r.status = exception ? RPGPU_V_READ_OFFSET_REGRESSION : ((bytes_consumed || benign) ? RPGPU_V_OK : err);
+            r.accepted = accepted < rd.desc_cap ? accepted : rd.desc_cap;
+            r.skipped = skipped;
+            r.bytes_consumed = bytes_consumed;
+            r.physical_offset = phys;
+            r.start_offset = start_offset;
+            r.cfg_bytes_consumed = cfg_bytes;
+            r.expected_next_batch = expected;
+            r.over_budget = over_budget;
+            r.stopped = stopped;
+            r.reserved0 = 0;
+            r.reserved1 = 0;
+            results[s] = r;
+        }
+    }
+}
+
+hipError_t launch_segment_parse(const uint8_t* d_data, const rpgpu_segment_read* d_reads, uint32_t n,
+                                rpgpu_segment_parse_result* d_res, rpgpu_batch_desc* d_descs,
+                                const uint32_t* d_tables, int grid, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t need = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+    const uint32_t g = (uint32_t)grid < need ? (uint32_t)grid : need;
+    segment_parse_kernel<<<g, kValidateThreads, 0, s>>>(d_data, d_reads, n, d_res, d_descs, d_tables);
+    return hipGetLastError();
+}
+
 // produce-handler error codes (rpgpu_kafka_error_codes_device)
 __global__ __launch_bounds__(256) void kafka_codes_kernel(const rpgpu_batch_result* __restrict__ res, uint32_t n,
                                                           uint32_t batch_max_bytes, int32_t* __restrict__ codes) {

@@ -259,6 +259,30 @@ class Engine:
                     states=d_states.cpu().numpy().view(abi.SEGMENT_STATE_DTYPE)[:ns].copy(),
                     entries=d_entries.cpu().numpy().view(abi.INDEX_ENTRY_DTYPE)[:n].copy())
 
+    # -- stream-level storage parser (rpgpu_segment_parse_device) ---------------------
+    def segment_parse(self, data: np.ndarray, reads: np.ndarray) -> dict:
+        """continuous_batch_parser::consume over each segment read on the GPU.
+        Returns host copies: results (per read), descs (the emitted slots)."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        reads = np.ascontiguousarray(reads, dtype=abi.SEGMENT_READ_DTYPE)
+        n = len(reads)
+        ncap = int((reads["desc_first"].astype(np.int64) + reads["desc_cap"]).max()) if n else 0
+        sh = torch.cuda.current_stream(dev).cuda_stream
+        d_data = torch.from_numpy(data.copy()).to(dev)
+        d_reads = torch.from_numpy(reads.view(np.uint8).copy()).to(dev)
+        d_res = torch.zeros(max(n, 1) * abi.SEGMENT_PARSE_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        d_descs = torch.zeros(max(ncap, 1) * 24, dtype=torch.uint8, device=dev)
+        rc = self._lib.rpgpu_segment_parse_device(self._ctx, d_data.data_ptr(), d_reads.data_ptr(), n,
+                                                  d_res.data_ptr(), d_descs.data_ptr(), sh)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_segment_parse_device: {rc} {self.last_error()}")
+        torch.cuda.synchronize(dev)
+        return dict(results=d_res.cpu().numpy().view(abi.SEGMENT_PARSE_RESULT_DTYPE)[:n].copy(),
+                    descs=d_descs.cpu().numpy().view(abi.DESC_DTYPE)[:ncap].copy())
+
     # -- synchronous scalar mirrors ---------------------------------------------------
     def uncompress(self, codec: int, data: bytes | np.ndarray, cap: int | None = None) -> tuple[int, bytes]:
         """compression::compressor::uncompress on the GPU: (verdict, bytes)."""
