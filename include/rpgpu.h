@@ -259,7 +259,8 @@ int32_t rpgpu_kafka_error_codes_device(rpgpu_ctx* ctx, const rpgpu_batch_result*
                                        uint32_t batch_max_bytes, int32_t* d_codes, void* hip_stream);
 
 /* Device-resident entry point: every pointer is device memory, the work is
- * enqueued on `hip_stream` (a hipStream_t; NULL = the context stream) and the
+ * enqueued on `hip_stream` (a hipStream_t; NULL = the context stream, a blocking
+ * stream ordered after the legacy default stream) and the
  * call returns without synchronising.  `d_scratch` must hold
  * rpgpu_validate_scratch_bytes(n) bytes.  *d_index_used receives the total
  * number of index entries reserved. */

@@ -182,7 +182,9 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
     int fit = 0;
     if (rpgpu::validate_occupancy(&fit) == hipSuccess && fit >= 1 && fit < bpc) bpc = fit;
     c->grid = c->cu_count * bpc;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    // a blocking stream: it orders after work on the legacy default stream (torch's
+    // current stream unless the caller set one), so NULL-stream calls are safe
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess) {
         delete c;
         return nullptr;
     }

@@ -238,7 +238,12 @@ struct WaveEmit {
         gbase = gend = dst + n;
     }
     // zstd literals
-    __device__ __forceinline__ uint8_t* litbuf(uint8_t*, uint64_t, uint64_t) { return scratch; }
+    // the buffer is reused block after block: sequences still pending read
+    // the previous block's literals, so they run first
+    __device__ __forceinline__ uint8_t* litbuf(uint8_t*, uint64_t, uint64_t) {
+        sync();
+        return scratch;
+    }
     __device__ __forceinline__ void litfill(uint8_t* d, uint8_t v, uint64_t n) { coop_fill(d, v, n, lid); }
     __device__ __forceinline__ bool huf1(const rpzstd::Ws& w, const uint8_t* src, uint64_t len, uint8_t* d,
                                          uint64_t n) {

@@ -16,6 +16,17 @@ class EngineError(RuntimeError):
     pass
 
 
+def _stream(stream: int):
+    """The HIP stream for a device call: the caller's, else torch's current
+    stream on the current device (the tensors' producer), never the context's
+    own non-blocking stream, which does not order after torch's work."""
+    if stream:
+        return stream
+    import torch
+
+    return torch.cuda.current_stream().cuda_stream or None
+
+
 class Engine:
     """One rpgpu context (one per Seastar shard x GPU in the reference's terms)."""
 
@@ -87,28 +98,28 @@ class Engine:
     def validate_device(self, d_descs: int, n: int, d_data: int, d_results: int, d_index: int,
                         index_cap: int, d_used: int, d_scratch: int, stream: int = 0) -> None:
         rc = self._lib.rpgpu_validate_device(self._ctx, d_descs, n, d_data, d_results, d_index,
-                                             index_cap, d_used, d_scratch, stream or None)
+                                             index_cap, d_used, d_scratch, _stream(stream))
         if rc != abi.RPGPU_OK:
             raise EngineError(f"rpgpu_validate_device: {rc} {self.last_error()}")
 
     def plan_device(self, d_descs: int, n: int, d_data: int, d_used: int, d_scratch: int,
                     stream: int = 0) -> None:
         rc = self._lib.rpgpu_plan_device(self._ctx, d_descs, n, d_data, d_used, d_scratch,
-                                         stream or None)
+                                         _stream(stream))
         if rc != abi.RPGPU_OK:
             raise EngineError(f"rpgpu_plan_device: {rc} {self.last_error()}")
 
     def run_device(self, d_descs: int, n: int, d_data: int, d_results: int, d_index: int,
                    index_cap: int, d_scratch: int, stream: int = 0) -> None:
         rc = self._lib.rpgpu_run_device(self._ctx, d_descs, n, d_data, d_results, d_index,
-                                        index_cap, d_scratch, stream or None)
+                                        index_cap, d_scratch, _stream(stream))
         if rc != abi.RPGPU_OK:
             raise EngineError(f"rpgpu_run_device: {rc} {self.last_error()}")
 
     def crc32c_ranges_device(self, d_data: int, d_off: int, d_len: int, d_seed: int, n: int,
                              d_out: int, stream: int = 0) -> None:
         rc = self._lib.rpgpu_crc32c_ranges_device(self._ctx, d_data, d_off, d_len, d_seed or None,
-                                                  n, d_out, stream or None)
+                                                  n, d_out, _stream(stream))
         if rc != abi.RPGPU_OK:
             raise EngineError(f"rpgpu_crc32c_ranges_device: {rc} {self.last_error()}")
 
@@ -120,7 +131,7 @@ class Engine:
     def decomp_plan_device(self, d_descs: int, n: int, d_data: int, d_results: int, d_out_bytes: int,
                            d_scratch: int, stream: int = 0) -> None:
         rc = self._lib.rpgpu_decomp_plan_device(self._ctx, d_descs, n, d_data, d_results, d_out_bytes,
-                                                d_scratch, stream or None)
+                                                d_scratch, _stream(stream))
         if rc != abi.RPGPU_OK:
             raise EngineError(f"rpgpu_decomp_plan_device: {rc} {self.last_error()}")
 
@@ -129,7 +140,7 @@ class Engine:
                           index_cap: int, d_used: int, d_scratch: int, stream: int = 0) -> None:
         rc = self._lib.rpgpu_decomp_run_device(self._ctx, d_descs, n, d_data, d_results, d_dres, d_out,
                                                out_cap, d_out_descs, d_out_results, d_index or None,
-                                               index_cap, d_used or None, d_scratch, stream or None)
+                                               index_cap, d_used or None, d_scratch, _stream(stream))
         if rc != abi.RPGPU_OK:
             raise EngineError(f"rpgpu_decomp_run_device: {rc} {self.last_error()}")
 

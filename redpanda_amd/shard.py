@@ -38,11 +38,11 @@ def partition_summaries_device(eng, d_descs, d_results, n: int, lo: int, hi: int
     import torch
 
     from . import abi
-    from .engine import EngineError
+    from .engine import EngineError, _stream
 
     out = torch.empty(hi - lo, NF, dtype=torch.int64, device=d_results.device)
     rc = abi.lib().rpgpu_partition_summaries_device(eng.ctx, d_descs.data_ptr(), d_results.data_ptr(), n, lo,
-                                                    hi - lo, out.data_ptr(), stream or None)
+                                                    hi - lo, out.data_ptr(), _stream(stream))
     if rc != abi.RPGPU_OK:
         raise EngineError(f"rpgpu_partition_summaries_device: {rc} {eng.last_error()}")
     return out

@@ -263,6 +263,7 @@ def test_gpu_recovery_pipeline(eng):
     rng = np.random.default_rng(32)
     segs = [s for s in corpus(rng) if not s[1]]
     data, reads = layout(segs)
+    reads["ops"] = abi.OP_CRC | abi.OP_HDRCRC  # the checksumming consumer: no record walk
     got = eng.segment_parse(data, reads)
     res = got["results"]
     descs = np.concatenate([got["descs"][int(r["desc_first"]):int(r["desc_first"]) + int(x["accepted"])]
