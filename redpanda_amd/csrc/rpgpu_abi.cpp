@@ -56,7 +56,7 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                              uint64_t out_cap, rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_vres2,
                              rpgpu_record_index* d_index, uint64_t index_cap, uint64_t* d_index_used,
                              void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s,
-                             const Overlap* ov);
+                             const Overlap* ov, const DecompStreams* ds);
 hipError_t launch_uncompress_bound(uint32_t codec, const uint8_t* d_in, uint64_t n, uint64_t* d_res,
                                    hipStream_t s);
 hipError_t launch_uncompress_one(uint32_t codec, const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint64_t cap,
@@ -114,6 +114,8 @@ struct rpgpu_ctx {
     hipStream_t stream = nullptr;
     rpgpu::Overlap overlap{};  // second stream + events: walks overlap checksums
     bool have_overlap = false;
+    rpgpu::DecompStreams dstreams{};  // large-batch wave decoders beside the lane decoders
+    bool have_dstreams = false;
     uint32_t* d_tables = nullptr;
     DevBuf work;     // submissions: descs | data | results | index | scratch | used
     DevBuf small;    // scalar mirrors
@@ -194,6 +196,9 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
         if (v >= 1 && v <= rpgpu::kMaxRunChunks) c->overlap.chunks = v;
     }
     c->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    c->have_dstreams = hipStreamCreateWithFlags(&c->dstreams.aux, hipStreamNonBlocking) == hipSuccess &&
+                       hipEventCreateWithFlags(&c->dstreams.fork, hipEventDisableTiming) == hipSuccess &&
+                       hipEventCreateWithFlags(&c->dstreams.join, hipEventDisableTiming) == hipSuccess;
     c->have_overlap = hipStreamCreateWithFlags(&c->overlap.aux, hipStreamNonBlocking) == hipSuccess;
     for (int k = 0; c->have_overlap && k <= c->overlap.chunks; k++)
         c->have_overlap = hipEventCreateWithFlags(&c->overlap.ev[k], hipEventDisableTiming) == hipSuccess;
@@ -231,6 +236,12 @@ void rpgpu_close(rpgpu_ctx* c) {
         if (c->overlap.ev[k]) (void)hipEventDestroy(c->overlap.ev[k]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->efd >= 0) close(c->efd);
+    if (c->dstreams.aux) {
+        (void)hipStreamSynchronize(c->dstreams.aux);
+        (void)hipStreamDestroy(c->dstreams.aux);
+    }
+    if (c->dstreams.fork) (void)hipEventDestroy(c->dstreams.fork);
+    if (c->dstreams.join) (void)hipEventDestroy(c->dstreams.join);
     delete c;
 }
 
@@ -354,7 +365,8 @@ int32_t rpgpu_decomp_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, u
     hipError_t e = rpgpu::launch_decomp_run(d_descs, n, d_data, d_results, d_dres, d_out, out_cap, d_out_descs,
                                             d_out_results, d_index, d_index ? index_cap : 0, d_index_used,
                                             d_scratch, c->d_tables, c->grid, s,
-                                            c->have_overlap ? &c->overlap : nullptr);
+                                            c->have_overlap ? &c->overlap : nullptr,
+                                            c->have_dstreams ? &c->dstreams : nullptr);
     if (e != hipSuccess) return fail(c, e, "decomp run launch");
     return RPGPU_OK;
 }

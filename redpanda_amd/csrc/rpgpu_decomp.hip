@@ -14,11 +14,16 @@
 //                        61-byte header + an upper bound of the decoded size
 //                        read off the frame's block headers / chunk
 //                        preambles + kSlack; exclusive scan of the slots
-//   decomp_wave_kernel   one wavefront per batch (persistent grid, batches
-//                        taken from an atomic counter): the codec's decisions
-//                        run uniformly in all lanes, the bytes are produced
-//                        by the wave 64 sequences at a time (rpgpu_wave.h);
-//                        zstd's Huffman / FSE tables live in LDS
+//   decomp_lane_kernel / zstd_lane_kernel
+//                        batches up to kLaneMaxSlot: one lane per batch runs
+//                        the codec restatement with direct copies; 64 batches
+//                        per wave keep the serial decode SIMD-efficient
+//   decomp_wave_kernel   larger batches, concurrently on a second stream:
+//                        one wavefront per batch (batches taken from an
+//                        atomic counter), the decisions uniform in all lanes,
+//                        the bytes produced by the wave 64 sequences at a
+//                        time (rpgpu_wave.h), zstd tables in LDS -- a 1 MiB
+//                        body no longer waits on one lane
 //   validate_kernel      over the rewritten batches with RPGPU_OP_RECRC: the
 //                        Kafka CRC of the decompressed body, then the header
 //                        CRC over the header carrying it; record walk; index
@@ -40,24 +45,32 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
 size_t validate_scratch_bytes(uint32_t n);
 
 namespace {
-// decoder wavefronts in flight: 8 per CU (the zstd workspace takes ~19 KB of
-// the 160 KiB LDS) on 256 CUs; each owns a literal scratch buffer
+// wave decoders in flight: 8 per CU (the zstd workspace takes ~19 KB of the
+// 160 KiB LDS) on 256 CUs; each owns a literal scratch buffer
 constexpr uint32_t kDecompWaves = 2048;
 constexpr uint64_t kLitScratch = (128u << 10) + 256;  // ZSTD_BLOCKSIZE_MAX + slack
+// lane zstd decoders in flight, each with its workspace in HBM
+#ifndef RPZ_LANES
+#define RPZ_LANES 131072  // 2 waves per SIMD at the lane kernel's VGPR count
+#endif
+constexpr uint32_t kZstdLanes = RPZ_LANES;
+uint32_t zstd_lanes(uint32_t n) { return n < kZstdLanes ? n : kZstdLanes; }
 uint32_t decomp_waves(uint32_t n) { return n < kDecompWaves ? n : kDecompWaves; }
 // scratch: slot[n] u64 | local[n] u64 | block_sum[nb] u64 | validate scratch |
-//          counter (256 B) | literal scratch[waves]
+//          counters (256 B) | wave literal scratch[waves] | zstd lane Ws[lanes]
 struct Parts {
     uint64_t *slot, *local, *block_sum;
     void* vscratch;
     uint32_t* counter;
     uint8_t* lits;
+    rpzstd::Ws* zws;
 };
 size_t parts_head(uint32_t n) {
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
     return ((size_t)n * 16 + nb * 8 + 255) & ~(size_t)255;
 }
 size_t counter_offset(uint32_t n) { return (parts_head(n) + validate_scratch_bytes(n) + 255) & ~(size_t)255; }
+size_t zws_offset(uint32_t n) { return counter_offset(n) + 256 + (size_t)decomp_waves(n) * kLitScratch; }
 Parts parts(void* p, uint32_t n) {
     uint8_t* b = static_cast<uint8_t*>(p);
     Parts s;
@@ -67,11 +80,16 @@ Parts parts(void* p, uint32_t n) {
     s.vscratch = b + parts_head(n);
     s.counter = reinterpret_cast<uint32_t*>(b + counter_offset(n));
     s.lits = b + counter_offset(n) + 256;
+    s.zws = reinterpret_cast<rpzstd::Ws*>(b + zws_offset(n));
     return s;
 }
 }  // namespace
 
-size_t decomp_scratch_bytes(uint32_t n) { return counter_offset(n) + 256 + (size_t)decomp_waves(n) * kLitScratch; }
+size_t decomp_scratch_bytes(uint32_t n) { return zws_offset(n) + (size_t)zstd_lanes(n) * sizeof(rpzstd::Ws); }
+
+// slots above this go to the wave decoders (a lane's serial decode of a
+// large body would hold up the whole launch)
+constexpr uint64_t kLaneMaxSlot = 256u << 10;
 
 // slot[i] of a batch whose bound exceeds the per-batch ceiling: no output
 // reserved (the scan counts 0), verdict DECOMP_OVERFLOW
@@ -185,6 +203,83 @@ __device__ __forceinline__ void finish_batch(uint32_t i, const rpgpu_batch_desc&
     out_descs[i] = od;
 }
 
+// the batch's output slot, or the verdict that it gets none
+__device__ __forceinline__ bool plan_slot(uint64_t& sz, uint64_t off, uint64_t out_cap, int32_t& verdict) {
+    if (sz == kOverCeiling) {
+        sz = 0;
+        verdict = RPGPU_V_DECOMP_OVERFLOW;
+        return false;
+    }
+    if (sz == 0) {
+        verdict = RPGPU_V_DECOMP_UNSUPPORTED;  // gzip
+        return false;
+    }
+    if (off + sz > out_cap) {
+        verdict = RPGPU_V_DECOMP_OVERFLOW;  // caller's buffer smaller than the plan
+        return false;
+    }
+    return true;
+}
+__device__ __forceinline__ bool wave_owned(const rpgpu_batch_desc& d, const rpgpu_batch_result& v, uint64_t sz) {
+    return decomp_wanted(d, v) && sz != kOverCeiling && sz > kLaneMaxSlot && (v.codec >= 2 && v.codec <= 4);
+}
+
+// LZ4 / snappy batches (and every batch nobody decodes: its verdict), one lane each
+__global__ __launch_bounds__(256) void decomp_lane_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
+    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
+    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
+    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
+    rpgpu_batch_desc* __restrict__ out_descs) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const rpgpu_batch_desc d = descs[i];
+    const rpgpu_batch_result v = vres[i];
+    const bool want = decomp_wanted(d, v);
+    uint64_t sz = slot[i];
+    if (want && (v.codec == 4 || wave_owned(d, v, sz))) return;  // zstd_lane_kernel / decomp_wave_kernel
+    const uint64_t off = block_base[i / kScanBlock] + local[i];
+    int32_t verdict = RPGPU_V_SKIPPED;
+    uint64_t len = 0;
+    if (want && plan_slot(sz, off, out_cap, verdict)) {
+        rpcodec::DirectEmit em;
+        verdict = rpcodec::uncompress(em, v.codec, data + d.offset + kHeaderSize,
+                                      (uint64_t)(uint32_t)v.size_bytes - kHeaderSize, out + off + kHeaderSize,
+                                      sz - kHeaderSize - rpcodec::kSlack, &len);
+    }
+    finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
+}
+
+// zstd batches up to kLaneMaxSlot: one lane per batch (grid-stride over
+// kZstdLanes lanes), each with its workspace (Huffman / FSE tables) in HBM.
+__global__ __launch_bounds__(256) void zstd_lane_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
+    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
+    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
+    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
+    rpgpu_batch_desc* __restrict__ out_descs, rpzstd::Ws* __restrict__ wsbuf) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lanes = gridDim.x * blockDim.x;
+    if (g >= n) return;  // lanes past the arena own no workspace
+    rpzstd::Ws& ws = wsbuf[g];
+    for (uint32_t i = g; i < n; i += lanes) {
+        const rpgpu_batch_desc d = descs[i];
+        const rpgpu_batch_result v = vres[i];
+        uint64_t sz = slot[i];
+        if (!decomp_wanted(d, v) || v.codec != 4 || wave_owned(d, v, sz)) continue;
+        const uint64_t off = block_base[i / kScanBlock] + local[i];
+        int32_t verdict = RPGPU_V_SKIPPED;
+        uint64_t len = 0;
+        if (plan_slot(sz, off, out_cap, verdict)) {
+            rpzstd::DirectEmit em;
+            verdict = rpzstd::uncompress(em, data + d.offset + kHeaderSize,
+                                         (uint64_t)(uint32_t)v.size_bytes - kHeaderSize, out + off + kHeaderSize,
+                                         sz - kHeaderSize - rpcodec::kSlack, &len, ws);
+        }
+        finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
+    }
+}
+
 // One batch body through the codec restatement, bytes produced by the wave.
 // K: the codec family a kernel instance decodes (kFamZstd: 4, kFamLz: 2 and 3).
 constexpr uint32_t kFamZstd = 4, kFamLz = 3;
@@ -215,7 +310,9 @@ __global__ __launch_bounds__(64) void decomp_wave_kernel(
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
     rpgpu_decomp_result* __restrict__ dres, uint8_t* out, uint64_t out_cap,
     rpgpu_batch_desc* __restrict__ out_descs, uint32_t* counter, uint8_t* lit_scratch) {
-    __shared__ rpzstd::Ws ws;
+    // the zstd workspace: dynamic LDS, sizeof(Ws) for the zstd instance, none for LZ
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+    rpzstd::Ws& ws = *reinterpret_cast<rpzstd::Ws*>(dyn_lds);
     const uint32_t lid = lane_id();
     rpwave::WaveEmit em;
     em.init(lit_scratch + (uint64_t)blockIdx.x * kLitScratch);
@@ -226,27 +323,16 @@ __global__ __launch_bounds__(64) void decomp_wave_kernel(
         if (i >= n) break;
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
-        const bool want = decomp_wanted(d, v);
-        // each batch has one owner: zstd batches the zstd instance, every
-        // other batch (LZ4, snappy, gzip, skipped) the LZ instance
-        if (FAM == kFamZstd ? !(want && v.codec == 4) : (want && v.codec == 4)) continue;
-        const uint64_t off = block_base[i / kScanBlock] + local[i];
         uint64_t sz = slot[i];
+        // the large batches of this instance's codec family; the lane kernels take the rest
+        if (!wave_owned(d, v, sz) || !in_family(FAM, v.codec)) continue;
+        const uint64_t off = block_base[i / kScanBlock] + local[i];
         int32_t verdict = RPGPU_V_SKIPPED;
         uint64_t len = 0;
-        if (want) {
-            if (sz == kOverCeiling) {
-                sz = 0;
-                verdict = RPGPU_V_DECOMP_OVERFLOW;
-            } else if (sz == 0) {
-                verdict = RPGPU_V_DECOMP_UNSUPPORTED;  // gzip
-            } else if (off + sz > out_cap) {
-                verdict = RPGPU_V_DECOMP_OVERFLOW;  // caller's buffer smaller than the plan
-            } else {
-                verdict = decode_body<FAM>(em, ws, v.codec, data + d.offset + kHeaderSize,
-                                      (uint64_t)(uint32_t)v.size_bytes - kHeaderSize, out + off + kHeaderSize,
-                                      sz - kHeaderSize - rpcodec::kSlack, &len);
-            }
+        if (plan_slot(sz, off, out_cap, verdict)) {
+            verdict = decode_body<FAM>(em, ws, v.codec, data + d.offset + kHeaderSize,
+                                       (uint64_t)(uint32_t)v.size_bytes - kHeaderSize, out + off + kHeaderSize,
+                                       sz - kHeaderSize - rpcodec::kSlack, &len);
         }
         if (lid == 0) finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
     }
@@ -305,19 +391,38 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                              uint64_t out_cap, rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_vres2,
                              rpgpu_record_index* d_index, uint64_t index_cap, uint64_t* d_index_used,
                              void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s,
-                             const Overlap* ov) {
+                             const Overlap* ov, const DecompStreams* ds) {
     if (n == 0) return d_index_used ? hipMemsetAsync(d_index_used, 0, sizeof(uint64_t), s) : hipSuccess;
     const Parts p = parts(d_scratch, n);
     const uint32_t nblk = (n + 255) / 256;
     hipError_t e = hipMemsetAsync(p.counter, 0, 2 * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
-    decomp_wave_kernel<kFamLz><<<decomp_waves(n), 64, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
-                                                             d_dres, d_out, out_cap, d_out_descs, p.counter, p.lits);
+    // large batches on the wave decoders, on a second stream beside the lanes
+    hipStream_t ws = s;
+    if (ds) {
+        if ((e = hipEventRecord(ds->fork, s)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(ds->aux, ds->fork, 0)) != hipSuccess) return e;
+        ws = ds->aux;
+    }
+    decomp_wave_kernel<kFamZstd><<<decomp_waves(n), 64, sizeof(rpzstd::Ws), ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
+                                                                p.block_sum, d_dres, d_out, out_cap, d_out_descs,
+                                                                p.counter + 1, p.lits);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    decomp_wave_kernel<kFamZstd><<<decomp_waves(n), 64, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
-                                                               p.block_sum, d_dres, d_out, out_cap, d_out_descs,
-                                                               p.counter + 1, p.lits);
+    decomp_wave_kernel<kFamLz><<<decomp_waves(n), 64, 0, ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
+                                                              p.block_sum, d_dres, d_out, out_cap, d_out_descs,
+                                                              p.counter, p.lits);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    decomp_lane_kernel<<<nblk, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
+                                            out_cap, d_out_descs);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint32_t zl = zstd_lanes(n);
+    zstd_lane_kernel<<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
+                                                      d_dres, d_out, out_cap, d_out_descs, p.zws);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (ds) {
+        if ((e = hipEventRecord(ds->join, ds->aux)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(s, ds->join, 0)) != hipSuccess) return e;
+    }
     if ((e = launch_plan(d_out_descs, n, d_out, d_index_used, p.vscratch, s)) != hipSuccess) return e;
     if ((e = launch_run(d_out_descs, n, d_out, d_vres2, d_index, index_cap, p.vscratch, d_tables, grid, s, ov)) !=
         hipSuccess)

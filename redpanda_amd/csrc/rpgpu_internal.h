@@ -47,6 +47,13 @@ struct Overlap {
     hipEvent_t ev[kMaxRunChunks + 1];
 };
 
+// rpgpu_decomp_run_device: the large batches' wave decoders run on `aux`
+// beside the lane decoders (fork / join events)
+struct DecompStreams {
+    hipStream_t aux;
+    hipEvent_t fork, join;
+};
+
 void build_tables(uint32_t* out /* kTableWords */);
 
 // Produce-handler verdict -> Kafka error code (produce.cc:440-489 in its

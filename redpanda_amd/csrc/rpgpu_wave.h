@@ -160,6 +160,7 @@ __device__ __forceinline__ void exec_group(uint8_t* gbase, uint32_t cnt, const u
 }
 
 struct WaveEmit {
+    static constexpr bool kInlineBlocks = true;
     // wave-uniform state
     uint8_t* gbase;      // output position of the group's first sequence
     uint8_t* gend;       // output position after the last sequence taken

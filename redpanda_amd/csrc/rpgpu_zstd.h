@@ -61,6 +61,11 @@
 // with the workspace in LDS: inlined, so its accesses stay ds_read / ds_write
 // (through a generic pointer they would become flat accesses).
 #define RPZ_COLD RPC_HD
+#if defined(__HIPCC__)
+#define RPZ_HD_NOINL __host__ __device__
+#else
+#define RPZ_HD_NOINL static
+#endif
 
 namespace rpzstd {
 
@@ -696,6 +701,7 @@ struct Huf4 {
 // emitter (rpgpu_wave.h) decodes the four streams on four lanes into a
 // scratch buffer and executes sequences 64 at a time with the whole wave.
 struct DirectEmit {
+    static constexpr bool kInlineBlocks = false;
     RPC_HD void lits(uint8_t* dst, const uint8_t* src, uint64_t n) { copy_lits(dst, src, n); }
     RPC_HD void match(uint8_t* dst, uint64_t off, uint64_t n) { copy_seq_match(dst, off, n); }
     RPC_HD void fill(uint8_t* dst, uint8_t v, uint64_t n) { fill_bytes(dst, v, n); }
@@ -1031,6 +1037,24 @@ RPZ_COLD int64_t block(E& em, Ws& w, const uint8_t* in, uint64_t n, uint8_t* out
     return (int64_t)(o - op);
 }
 
+// block() out of line for the lane decoders (DirectEmit: inlined at both call
+// sites the lane kernel outgrew the instruction cache), inline for the wave
+// emitter (its state stays in registers, its workspace accesses LDS ops).
+template <class E>
+__attribute__((noinline)) RPZ_HD_NOINL int64_t block_noinline(E& em, Ws& w, const uint8_t* in, uint64_t n,
+                                                              uint8_t* out, uint64_t fstart, uint64_t op,
+                                                              uint64_t cap, uint64_t tail) {
+    return block(em, w, in, n, out, fstart, op, cap, tail);
+}
+template <class E>
+RPC_HD int64_t block_call(E& em, Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t fstart, uint64_t op,
+                          uint64_t cap, uint64_t tail) {
+    if constexpr (E::kInlineBlocks)
+        return block(em, w, in, n, out, fstart, op, cap, tail);
+    else
+        return block_noinline(em, w, in, n, out, fstart, op, cap, tail);
+}
+
 // ------------------------------------------------------------------ XXH64
 constexpr uint64_t kQ1 = 11400714785074694791ull, kQ2 = 14029467366897019727ull, kQ3 = 1609587929392839161ull,
                    kQ4 = 9650029242287828579ull, kQ5 = 2870177450012600261ull;
@@ -1224,7 +1248,7 @@ RPC_HD int32_t uncompress_impl(E& em, const uint8_t* in, uint64_t n, uint8_t* ou
                 if (type == 2) {
                     if (T > cap) return V_OVERFLOW;
                     const uint64_t lim = fend < cap ? fend : cap;
-                    r = block(em, w, f + ip, size, out, fstart, T, lim - T, cap);
+                    r = block_call(em, w, f + ip, size, out, fstart, T, lim - T, cap);
                     if (r == -2 || (r < 0 && lim < fend)) return fend <= cap ? V_ERROR : V_OVERFLOW;
                     if (r < 0) return RPZ_FAIL(V_ERROR);
                     ip += size;
@@ -1305,7 +1329,7 @@ RPC_HD int32_t uncompress_impl(E& em, const uint8_t* in, uint64_t n, uint8_t* ou
                     if (avail < size) break;  // waits in the load stage
                     if (T > cap) return V_OVERFLOW;
                     const uint64_t lim = room_ring < cap - T ? room_ring : cap - T;
-                    const int64_t rr = block(em, w, f + ip, size, out, fstart, T, lim, cap);
+                    const int64_t rr = block_call(em, w, f + ip, size, out, fstart, T, lim, cap);
                     if (rr == -2 || (rr < 0 && lim < room_ring)) {
                         // the slot, not the library, ran out: decide with the bound
                         return V_OVERFLOW;
