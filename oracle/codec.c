@@ -10,6 +10,7 @@
  *   zstd  compression/stream_zstd.cc:29-87,153-223
  *   snappy-java compression/internal/snappy_java_compressor.cc:76-110
  *         -> compression/snappy_standard_compressor.cc:102-160
+ *   gzip  compression/internal/gzip_compressor.cc:89-104,177-229 (zlib 1.2.11)
  *   dispatch compression/compression.cc:35-55
  * Compression follows lz4_frame_compressor.cc:68-158 (independent blocks,
  * content size, level 1), stream_zstd.cc:89-151 (pledged size, level 3
@@ -21,6 +22,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <zstd.h>
+#include <zlib.h>
 #include <zstd_errors.h>
 
 #include "rporacle.h"
@@ -197,6 +199,45 @@ static int32_t snappy_java_uncompress(const uint8_t* x, size_t n, struct sink* s
     return RPGPU_V_OK;
 }
 
+/* gzip_compressor::uncompress (internal/gzip_compressor.cc:89-104,177-229):
+ * inflateInit2(15 + 32), inflateGetHeader, then inflate(Z_NO_FLUSH) into
+ * chunks of min(128 KiB, 2 * previous) (first min(128 KiB, 3 n) * 2) while it
+ * returns Z_OK with input left.  Errors throw runtime_error.  The reference's
+ * gz_header is uninitialised (FEXTRA / FNAME / FCOMMENT then go through
+ * garbage pointers: undefined); here it is zeroed, so those fields are skipped. */
+static int32_t gzip_uncompress(const uint8_t* in, size_t n, struct sink* s) {
+    z_stream zs;
+    memset(&zs, 0, sizeof(zs));
+    zs.next_in = (unsigned char*)in;
+    zs.avail_in = (uInt)n;
+    if (inflateInit2(&zs, 15 + 32) != Z_OK) return RPGPU_V_DECOMP_ERROR;
+    gz_header hdr;
+    memset(&hdr, 0, sizeof(hdr));
+    if (inflateGetHeader(&zs, &hdr) != Z_OK) {
+        inflateEnd(&zs);
+        return RPGPU_V_DECOMP_ERROR;
+    }
+    size_t chunk = n * 3 < MAX_CHUNK ? n * 3 : MAX_CHUNK;
+    int code;
+    uint8_t* tmp = (uint8_t*)malloc(MAX_CHUNK);
+    do {
+        chunk = chunk * 2 < MAX_CHUNK ? chunk * 2 : MAX_CHUNK;
+        zs.next_out = tmp;
+        zs.avail_out = (uInt)chunk;
+        code = inflate(&zs, Z_NO_FLUSH);
+        if (code == Z_STREAM_ERROR || code == Z_NEED_DICT || code == Z_DATA_ERROR || code == Z_MEM_ERROR) {
+            free(tmp);
+            inflateEnd(&zs);
+            return RPGPU_V_DECOMP_ERROR;
+        }
+        sink_append(s, tmp, chunk - zs.avail_out);
+    } while (code == Z_OK && zs.avail_in > 0);
+    free(tmp);
+    inflateEnd(&zs);
+    if (code != Z_OK && code != Z_STREAM_END) return RPGPU_V_DECOMP_ERROR;
+    return RPGPU_V_OK;
+}
+
 int32_t orc_uncompress(int codec, const uint8_t* in, size_t n, uint8_t* out, size_t cap,
                        size_t* out_len) {
     struct sink s = {out, cap, 0, 0};
@@ -209,7 +250,7 @@ int32_t orc_uncompress(int codec, const uint8_t* in, size_t n, uint8_t* out, siz
     case 2: v = snappy_java_uncompress(in, n, &s); break;
     case 3: v = lz4_uncompress(in, n, &s); break;
     case 4: v = zstd_uncompress(in, n, &s); break;
-    case 1: v = RPGPU_V_DECOMP_UNSUPPORTED; break; /* gzip: not in any config */
+    case 1: v = gzip_uncompress(in, n, &s); break;
     default: v = RPGPU_V_DECOMP_ERROR; break;      /* none: "nothing to uncompress" */
     }
     *out_len = s.len;
@@ -228,6 +269,7 @@ size_t orc_compress_bound(int codec, size_t n) {
         return LZ4F_compressFrameBound(n, &prefs) + 64;
     }
     case 4: return ZSTD_compressBound(n) + 64;
+    case 1: return compressBound(n) + 64;
     case 2: return snappy_max_compressed_length(n) + 64 + 4 * (n / MAX_CHUNK + 1);
     default: return n + 64;
     }
@@ -287,6 +329,20 @@ int32_t orc_compress(int codec, const uint8_t* in, size_t n, uint8_t* out, size_
         }
         *out_len = pos;
         return RPGPU_V_OK;
+    }
+    case 1: { /* gzip_compressor::compress (gzip_compressor.cc:128-172): gzip wrapper, level -1 */
+        z_stream zs;
+        memset(&zs, 0, sizeof(zs));
+        if (deflateInit2(&zs, Z_DEFAULT_COMPRESSION, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK)
+            return RPGPU_V_DECOMP_ERROR;
+        zs.next_in = (unsigned char*)in;
+        zs.avail_in = (uInt)n;
+        zs.next_out = out;
+        zs.avail_out = (uInt)cap;
+        int r = deflate(&zs, Z_FINISH);
+        *out_len = zs.total_out;
+        deflateEnd(&zs);
+        return r == Z_STREAM_END ? RPGPU_V_OK : RPGPU_V_DECOMP_ERROR;
     }
     default: return RPGPU_V_DECOMP_UNSUPPORTED;
     }

@@ -34,6 +34,13 @@
 #else
 #define RPC_HD static inline
 #endif
+// member functions (a static specifier does not apply to them on the host)
+#if defined(__HIPCC__)
+#define RPC_MF __host__ __device__ __forceinline__
+#else
+#define RPC_MF inline
+#endif
+
 
 namespace rpcodec {
 

@@ -1,4 +1,5 @@
-"""The engine's decoder restatements (rpgpu_codec.h, rpgpu_zstd.h: the code the
+"""The engine's decoder restatements (rpgpu_codec.h, rpgpu_zstd.h,
+rpgpu_inflate.h: the code the
 GPU kernels run) built for the host with AddressSanitizer and
 UndefinedBehaviorSanitizer, run over the differential fuzz corpora with the
 device's exact buffer geometry (--exact 1: RPGPU_ARENA_TAIL_PAD readable
@@ -51,3 +52,8 @@ def test_codec_restatement_asan_ubsan(tmp_path, seed):
 @pytest.mark.parametrize("seed", [41])
 def test_zstd_restatement_asan_ubsan(tmp_path, seed):
     run(build(tmp_path, "zstd_fuzz", [f"{CONDA}/lib/libzstd.so"]), 250, seed, tmp_path)
+
+
+@pytest.mark.parametrize("seed", [61])
+def test_inflate_restatement_asan_ubsan(tmp_path, seed):
+    run(build(tmp_path, "inflate_fuzz", [f"{CONDA}/lib/libz.so"]), 2000, seed, tmp_path)
