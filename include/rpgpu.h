@@ -91,7 +91,7 @@ enum rpgpu_verdict {
      * 8 MiB workspace cannot hold is RPGPU_V_DECOMP_ERROR like every other
      * zstd error. */
     RPGPU_V_LZ4_TRAILING = 32,     /* unconsumed input after LZ4 frame end        */
-    RPGPU_V_DECOMP_UNSUPPORTED = 33,/* codec not implemented on this engine (gzip) */
+    RPGPU_V_DECOMP_UNSUPPORTED = 33,/* reserved: every codec 1..4 is decoded     */
     RPGPU_V_DECOMP_OVERFLOW = 34,  /* decompressed size exceeds the output slot, or
                                       its bound exceeds opts.max_decoded_batch */
     /* multi-batch record sets (kafka/protocol/batch_reader.cc:50-58) */
@@ -325,7 +325,7 @@ int32_t rpgpu_crc_record_batch(rpgpu_ctx* ctx, const rpgpu_rp_header* h,
  * internal_header_only_crc.  A truncated frame yields the partial output with
  * RPGPU_V_OK, as the reference does. */
 typedef struct rpgpu_decomp_result {
-    int32_t verdict;     /* OK, DECOMP_ERROR, LZ4_TRAILING, DECOMP_UNSUPPORTED,
+    int32_t verdict;     /* OK, DECOMP_ERROR, LZ4_TRAILING,
                             DECOMP_OVERFLOW, REC_UNDEFINED (snappy-java chunk
                             length with bit 31 set), SKIPPED                  */
     uint32_t codec;      /* attrs & 7 of the input batch                      */

@@ -170,7 +170,7 @@ def compress(codec: int, data) -> bytes:
 
 
 def decompress_arena(data: np.ndarray, descs: np.ndarray, results: np.ndarray, caps,
-                     codecs=(2, 3), nthreads: int = 1, out: np.ndarray | None = None,
+                     codecs=(1, 2, 3, 4), nthreads: int = 1, out: np.ndarray | None = None,
                      fast_crc: bool = False) -> dict:
     """Reference outcome of the decompress path for an arena already validated
     (`results` = validate_arena's or the engine's validation results, which
@@ -178,8 +178,8 @@ def decompress_arena(data: np.ndarray, descs: np.ndarray, results: np.ndarray, c
     (storage/parser_utils.cc:52-68,122-128) per batch with RPGPU_OP_DECOMP,
     verdict OK and a codec, then the rewritten batches through validate_arena
     as on-disk batches.  caps[i] = decoded-body capacity for batch i; codecs
-    outside `codecs` report RPGPU_V_DECOMP_UNSUPPORTED (33), as the engine
-    does for zstd/gzip."""
+    outside `codecs` report RPGPU_V_DECOMP_UNSUPPORTED (33) (the engine
+    decodes all four; the mask narrows a CPU baseline to a workload's codecs)."""
     data = np.ascontiguousarray(data, dtype=np.uint8)
     descs = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
     results = np.ascontiguousarray(results, dtype=RESULT_DTYPE)

@@ -59,7 +59,7 @@ def build_rpgen(force: bool = False) -> Path:
               f"-I{INCLUDE}", f"-I{CSRC}", f"-I{CONDA / 'include'}",
               *[str(CSRC / s) for s in RPGEN_SRCS],
               f"-L{CONDA / 'lib'}", f"-Wl,-rpath,{CONDA / 'lib'}",
-              "-llz4", "-lzstd", "-lsnappy", "-o", str(tmp)])
+              "-llz4", "-lzstd", "-lsnappy", "-lz", "-o", str(tmp)])
         os.replace(tmp, LIBRPGEN)
     return LIBRPGEN
 

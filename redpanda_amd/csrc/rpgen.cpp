@@ -19,6 +19,7 @@
 #include <snappy-c.h>
 #include <stdint.h>
 #include <string.h>
+#include <zlib.h>
 #include <zstd.h>
 
 #include <algorithm>
@@ -177,10 +178,10 @@ Plan plan_batch(const rpgen_spec& sp, uint64_t i) {
     p.hv_len = sp.header_value_len;
     p.codec = sp.codec;
     if (sp.codec_mix) {
-        static const uint8_t codecs[4] = {0, 2, 3, 4};  // none, snappy, lz4, zstd
-        uint32_t choices[4];
+        static const uint8_t codecs[5] = {0, 1, 2, 3, 4};  // none, gzip, snappy, lz4, zstd
+        uint32_t choices[5];
         int nc = 0;
-        for (int k = 0; k < 4; k++)
+        for (int k = 0; k < 5; k++)
             if (sp.codec_mix & (1u << codecs[k])) choices[nc++] = codecs[k];
         p.codec = nc ? (uint8_t)choices[r.below(nc)] : 0;
     }
@@ -291,6 +292,22 @@ bool compress_body(uint8_t codec, const std::vector<uint8_t>& in, std::vector<ui
         ZSTD_freeCCtx(c);
         if (ZSTD_isError(r)) return false;
         out.resize(ob.pos);
+        return true;
+    }
+    case 1: {  // gzip_compressor.cc:25-90 (deflateInit2 default level, gzip wrapper)
+        z_stream zs;
+        memset(&zs, 0, sizeof(zs));
+        if (deflateInit2(&zs, Z_DEFAULT_COMPRESSION, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
+        out.resize(deflateBound(&zs, n) + 64);
+        zs.next_in = const_cast<Bytef*>(in.data());
+        zs.avail_in = (uInt)n;
+        zs.next_out = out.data();
+        zs.avail_out = (uInt)out.size();
+        const int r = deflate(&zs, Z_FINISH);
+        const size_t len = zs.total_out;
+        deflateEnd(&zs);
+        if (r != Z_STREAM_END) return false;
+        out.resize(len);
         return true;
     }
     case 2: {  // snappy_java_compressor.cc:58-75

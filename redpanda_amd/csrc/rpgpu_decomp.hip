@@ -10,14 +10,18 @@
 // and indexed like those of any other batch.
 //
 // After validation of the compressed arena (validate_kernel):
+//   gzip_bound_kernel    one lane per gzip batch: the exact decoded size by a
+//                        counting decode (deflate has no size preamble)
 //   decomp_caps_kernel   one thread per batch: the batch's output slot =
 //                        61-byte header + an upper bound of the decoded size
 //                        read off the frame's block headers / chunk
-//                        preambles + kSlack; exclusive scan of the slots
-//   decomp_lane_kernel / zstd_lane_kernel
-//                        batches up to kLaneMaxSlot: one lane per batch runs
-//                        the codec restatement with direct copies; 64 batches
-//                        per wave keep the serial decode SIMD-efficient
+//                        preambles (gzip: the counted size) + kSlack;
+//                        exclusive scan of the slots
+//   decomp_lane_kernel / ws_lane_kernel
+//                        batches up to kLaneMaxSlot (gzip: all of them): one
+//                        lane per batch runs the codec restatement with direct
+//                        copies; 64 batches per wave keep the serial decode
+//                        SIMD-efficient
 //   decomp_wave_kernel   larger batches, concurrently on a second stream:
 //                        one wavefront per batch (batches taken from an
 //                        atomic counter), the decisions uniform in all lanes,
@@ -32,6 +36,7 @@
 #include "rpgpu_codec.h"
 #include "rpgpu_zstd.h"
 #include "rpgpu_wave.h"
+#include "rpgpu_inflate.h"
 
 namespace rpgpu {
 
@@ -49,7 +54,7 @@ namespace {
 // 160 KiB LDS) on 256 CUs; each owns a literal scratch buffer
 constexpr uint32_t kDecompWaves = 2048;
 constexpr uint64_t kLitScratch = (128u << 10) + 256;  // ZSTD_BLOCKSIZE_MAX + slack
-// lane zstd decoders in flight, each with its workspace in HBM
+// lane zstd / gzip decoders in flight, each with its workspace in HBM
 #ifndef RPZ_LANES
 #define RPZ_LANES 131072  // 2 waves per SIMD at the lane kernel's VGPR count
 #endif
@@ -57,13 +62,17 @@ constexpr uint32_t kZstdLanes = RPZ_LANES;
 uint32_t zstd_lanes(uint32_t n) { return n < kZstdLanes ? n : kZstdLanes; }
 uint32_t decomp_waves(uint32_t n) { return n < kDecompWaves ? n : kDecompWaves; }
 // scratch: slot[n] u64 | local[n] u64 | block_sum[nb] u64 | validate scratch |
-//          counters (256 B) | wave literal scratch[waves] | zstd lane Ws[lanes]
+//          counters (256 B) | wave literal scratch[waves] | lane Ws[lanes]
+union LaneWs {
+    rpzstd::Ws z;
+    rpinfl::Ws g;
+};
 struct Parts {
     uint64_t *slot, *local, *block_sum;
     void* vscratch;
     uint32_t* counter;
     uint8_t* lits;
-    rpzstd::Ws* zws;
+    LaneWs* zws;
 };
 size_t parts_head(uint32_t n) {
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
@@ -80,12 +89,12 @@ Parts parts(void* p, uint32_t n) {
     s.vscratch = b + parts_head(n);
     s.counter = reinterpret_cast<uint32_t*>(b + counter_offset(n));
     s.lits = b + counter_offset(n) + 256;
-    s.zws = reinterpret_cast<rpzstd::Ws*>(b + zws_offset(n));
+    s.zws = reinterpret_cast<LaneWs*>(b + zws_offset(n));
     return s;
 }
 }  // namespace
 
-size_t decomp_scratch_bytes(uint32_t n) { return zws_offset(n) + (size_t)zstd_lanes(n) * sizeof(rpzstd::Ws); }
+size_t decomp_scratch_bytes(uint32_t n) { return zws_offset(n) + (size_t)zstd_lanes(n) * sizeof(LaneWs); }
 
 // slots above this go to the wave decoders (a lane's serial decode of a
 // large body would hold up the whole launch)
@@ -97,6 +106,28 @@ constexpr uint64_t kOverCeiling = 1ull << 63;
 
 __device__ __forceinline__ bool decomp_wanted(const rpgpu_batch_desc& d, const rpgpu_batch_result& v) {
     return (d.ops & RPGPU_OP_DECOMP) && v.verdict == RPGPU_V_OK && v.codec != 0;
+}
+
+__device__ __forceinline__ uint64_t body_len(const rpgpu_batch_result& v) {
+    return (uint64_t)(uint32_t)v.size_bytes - kHeaderSize;  // verdict OK: 61 <= size_bytes <= length
+}
+
+// gzip: the decoded size is only known by decoding (a count, no stores), one
+// lane per batch with its Huffman tables in HBM; left in slot[i] for the caps
+__global__ __launch_bounds__(256) void gzip_bound_kernel(const rpgpu_batch_desc* __restrict__ descs, uint32_t n,
+                                                         const uint8_t* __restrict__ data,
+                                                         const rpgpu_batch_result* __restrict__ vres,
+                                                         uint64_t* __restrict__ slot, LaneWs* __restrict__ wsbuf) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lanes = gridDim.x * blockDim.x;
+    if (g >= n) return;
+    rpinfl::Ws& ws = wsbuf[g].g;
+    for (uint32_t i = g; i < n; i += lanes) {
+        const rpgpu_batch_desc d = descs[i];
+        const rpgpu_batch_result v = vres[i];
+        if (!decomp_wanted(d, v) || v.codec != 1) continue;
+        slot[i] = rpinfl::bound(data + d.offset + kHeaderSize, body_len(v), ws);
+    }
 }
 
 // output slot per batch + exclusive scan within blocks of kScanBlock batches
@@ -111,11 +142,12 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
     if (i < n) {
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
-        if (decomp_wanted(d, v) && (v.codec == 2 || v.codec == 3 || v.codec == 4)) {
-            // verdict OK: kHeaderSize <= size_bytes <= descriptor length
-            const uint64_t body = (uint64_t)(uint32_t)v.size_bytes - kHeaderSize;
+        if (decomp_wanted(d, v)) {  // codec 1..4 (validation rejects 5..7)
+            const uint64_t body = body_len(v);
             const uint8_t* b = data + d.offset + kHeaderSize;
-            const uint64_t bound = v.codec == 4 ? rpzstd::bound(b, body) : rpcodec::uncompress_bound(v.codec, b, body);
+            const uint64_t bound = v.codec == 1   ? slot[i]  // gzip_bound_kernel's count
+                                   : v.codec == 4 ? rpzstd::bound(b, body)
+                                                  : rpcodec::uncompress_bound(v.codec, b, body);
             sz = (kHeaderSize + bound + rpcodec::kSlack + 15) & ~(uint64_t)15;
             if (bound > max_decoded || sz > max_decoded) {
                 sz = 0;
@@ -210,8 +242,8 @@ __device__ __forceinline__ bool plan_slot(uint64_t& sz, uint64_t off, uint64_t o
         verdict = RPGPU_V_DECOMP_OVERFLOW;
         return false;
     }
-    if (sz == 0) {
-        verdict = RPGPU_V_DECOMP_UNSUPPORTED;  // gzip
+    if (sz == 0) {  // no slot planned (not a codec 1..4 batch)
+        verdict = RPGPU_V_DECOMP_ERROR;
         return false;
     }
     if (off + sz > out_cap) {
@@ -224,7 +256,8 @@ __device__ __forceinline__ bool wave_owned(const rpgpu_batch_desc& d, const rpgp
     return decomp_wanted(d, v) && sz != kOverCeiling && sz > kLaneMaxSlot && (v.codec >= 2 && v.codec <= 4);
 }
 
-// LZ4 / snappy batches (and every batch nobody decodes: its verdict), one lane each
+// LZ4 / snappy batches up to kLaneMaxSlot (and every batch nobody decodes: its
+// verdict), one lane each
 __global__ __launch_bounds__(256) void decomp_lane_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
     const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
@@ -237,44 +270,52 @@ __global__ __launch_bounds__(256) void decomp_lane_kernel(
     const rpgpu_batch_result v = vres[i];
     const bool want = decomp_wanted(d, v);
     uint64_t sz = slot[i];
-    if (want && (v.codec == 4 || wave_owned(d, v, sz))) return;  // zstd_lane_kernel / decomp_wave_kernel
+    if (want && (v.codec == 4 || v.codec == 1 || wave_owned(d, v, sz))) return;  // ws_lane_kernel / decomp_wave_kernel
     const uint64_t off = block_base[i / kScanBlock] + local[i];
     int32_t verdict = RPGPU_V_SKIPPED;
     uint64_t len = 0;
     if (want && plan_slot(sz, off, out_cap, verdict)) {
         rpcodec::DirectEmit em;
-        verdict = rpcodec::uncompress(em, v.codec, data + d.offset + kHeaderSize,
-                                      (uint64_t)(uint32_t)v.size_bytes - kHeaderSize, out + off + kHeaderSize,
-                                      sz - kHeaderSize - rpcodec::kSlack, &len);
+        verdict = rpcodec::uncompress(em, v.codec, data + d.offset + kHeaderSize, body_len(v),
+                                      out + off + kHeaderSize, sz - kHeaderSize - rpcodec::kSlack, &len);
     }
     finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
 }
 
-// zstd batches up to kLaneMaxSlot: one lane per batch (grid-stride over
-// kZstdLanes lanes), each with its workspace (Huffman / FSE tables) in HBM.
-__global__ __launch_bounds__(256) void zstd_lane_kernel(
+// zstd batches up to kLaneMaxSlot (FAM 4) / all gzip batches (FAM 1): one lane
+// per batch (grid-stride over kZstdLanes lanes), each with its workspace
+// (Huffman / FSE tables) in HBM.  gzip is decoded bit-serially as zlib does;
+// no benchmark configuration carries it, so it has no wave
+// decoder.  One instance per codec keeps each at its own register count.
+template <uint32_t FAM>
+__global__ __launch_bounds__(256) void ws_lane_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
     const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
     rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
-    rpgpu_batch_desc* __restrict__ out_descs, rpzstd::Ws* __restrict__ wsbuf) {
+    rpgpu_batch_desc* __restrict__ out_descs, LaneWs* __restrict__ wsbuf) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lanes = gridDim.x * blockDim.x;
     if (g >= n) return;  // lanes past the arena own no workspace
-    rpzstd::Ws& ws = wsbuf[g];
+    LaneWs& ws = wsbuf[g];
     for (uint32_t i = g; i < n; i += lanes) {
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
         uint64_t sz = slot[i];
-        if (!decomp_wanted(d, v) || v.codec != 4 || wave_owned(d, v, sz)) continue;
+        if (!decomp_wanted(d, v) || v.codec != FAM || wave_owned(d, v, sz)) continue;
         const uint64_t off = block_base[i / kScanBlock] + local[i];
         int32_t verdict = RPGPU_V_SKIPPED;
         uint64_t len = 0;
         if (plan_slot(sz, off, out_cap, verdict)) {
-            rpzstd::DirectEmit em;
-            verdict = rpzstd::uncompress(em, data + d.offset + kHeaderSize,
-                                         (uint64_t)(uint32_t)v.size_bytes - kHeaderSize, out + off + kHeaderSize,
-                                         sz - kHeaderSize - rpcodec::kSlack, &len, ws);
+            const uint8_t* in = data + d.offset + kHeaderSize;
+            uint8_t* o = out + off + kHeaderSize;
+            const uint64_t cap = sz - kHeaderSize - rpcodec::kSlack;
+            if (FAM == 4) {
+                rpzstd::DirectEmit em;
+                verdict = rpzstd::uncompress(em, in, body_len(v), o, cap, &len, ws.z);
+            } else {
+                verdict = rpinfl::uncompress(in, body_len(v), o, cap, &len, ws.g);
+            }
         }
         finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
     }
@@ -330,9 +371,8 @@ __global__ __launch_bounds__(64) void decomp_wave_kernel(
         int32_t verdict = RPGPU_V_SKIPPED;
         uint64_t len = 0;
         if (plan_slot(sz, off, out_cap, verdict)) {
-            verdict = decode_body<FAM>(em, ws, v.codec, data + d.offset + kHeaderSize,
-                                       (uint64_t)(uint32_t)v.size_bytes - kHeaderSize, out + off + kHeaderSize,
-                                       sz - kHeaderSize - rpcodec::kSlack, &len);
+            verdict = decode_body<FAM>(em, ws, v.codec, data + d.offset + kHeaderSize, body_len(v),
+                                       out + off + kHeaderSize, sz - kHeaderSize - rpcodec::kSlack, &len);
         }
         if (lid == 0) finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
     }
@@ -349,10 +389,14 @@ __global__ __launch_bounds__(256) void decomp_patch_kernel(const rpgpu_decomp_re
     put_le(o, 17, vres2[i].crc, 4);
 }
 
-// scalar mirror (rpgpu_uncompress): the bound in one lane, the decode in one wave
+// scalar mirror (rpgpu_uncompress): the bound in one lane, the decode in one
+// wave (gzip: one lane)
 __global__ void uncompress_bound_kernel(uint32_t codec, const uint8_t* in, uint64_t n, uint64_t* res) {
+    __shared__ rpinfl::Ws gws;
     if (blockIdx.x == 0 && threadIdx.x == 0)
-        res[0] = codec == 4 ? (n ? rpzstd::bound(in, n) : 0) : rpcodec::uncompress_bound(codec, in, n);
+        res[0] = codec == 4   ? (n ? rpzstd::bound(in, n) : 0)
+                 : codec == 1 ? rpinfl::bound(in, n, gws)
+                              : rpcodec::uncompress_bound(codec, in, n);
 }
 __global__ __launch_bounds__(64) void uncompress_one_kernel(uint32_t codec, const uint8_t* in, uint64_t n,
                                                             uint8_t* out, uint64_t cap, uint64_t* res,
@@ -365,7 +409,11 @@ __global__ __launch_bounds__(64) void uncompress_one_kernel(uint32_t codec, cons
     if (n == 0) v = RPGPU_V_DECOMP_ERROR;  // "Asked to decompress an empty buffer"
     else if (codec == 4) v = decode_body<kFamZstd>(em, ws, codec, in, n, out, cap, &len);
     else if (codec == 2 || codec == 3) v = decode_body<kFamLz>(em, ws, codec, in, n, out, cap, &len);
-    else v = codec == 1 ? RPGPU_V_DECOMP_UNSUPPORTED : RPGPU_V_DECOMP_ERROR;
+    else if (codec == 1) {
+        __shared__ rpinfl::Ws gws;
+        v = RPGPU_V_DECOMP_ERROR;
+        if (lane_id() == 0) v = rpinfl::uncompress(in, n, out, cap, &len, gws);
+    } else v = RPGPU_V_DECOMP_ERROR;
     if (lane_id() == 0) {
         res[1] = (uint64_t)(int64_t)v;
         res[2] = len;
@@ -379,9 +427,13 @@ hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const
     if (n == 0) return d_out_bytes ? hipMemsetAsync(d_out_bytes, 0, sizeof(uint64_t), s) : hipSuccess;
     const Parts p = parts(d_scratch, n);
     const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
+    const uint32_t zl = zstd_lanes(n);
+    gzip_bound_kernel<<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.zws);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
     decomp_caps_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
                                                  max_decoded);
-    hipError_t e = hipGetLastError();
+    e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_block_scan(p.block_sum, nb, d_out_bytes, s);
 }
@@ -416,8 +468,11 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                                             out_cap, d_out_descs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t zl = zstd_lanes(n);
-    zstd_lane_kernel<<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
-                                                      d_dres, d_out, out_cap, d_out_descs, p.zws);
+    ws_lane_kernel<4><<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
+                                                         d_dres, d_out, out_cap, d_out_descs, p.zws);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    ws_lane_kernel<1><<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
+                                                         d_dres, d_out, out_cap, d_out_descs, p.zws);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ds) {
         if ((e = hipEventRecord(ds->join, ds->aux)) != hipSuccess) return e;

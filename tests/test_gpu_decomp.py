@@ -1,7 +1,7 @@
 """GPU parity of the decompress path (rpgpu_decomp_plan_device /
 rpgpu_decomp_run_device and the rpgpu_uncompress scalar mirror) against the
 oracle: compression::compressor::uncompress (compression/compression.cc:35-55)
-over liblz4 / snappy / libzstd through the reference's wrapper loops, the batch rewrite
+over zlib / liblz4 / snappy / libzstd through the reference's wrapper loops, the batch rewrite
 of maybe_decompress_batch_sync (storage/parser_utils.cc:52-68,122-128) and the
 record walk of the rewritten batches.  Compared per batch: decompress verdict,
 decoded length, the rewritten batch's bytes (header with fresh CRCs + body),
@@ -29,7 +29,7 @@ def compare(got, data, descs):
     wres, _, _ = orc.validate_arena(data, descs)
     assert np.array_equal(res.view(np.uint8), wres.view(np.uint8)), "validation results differ"
     caps = np.where(dres["out_cap"] > 0, dres["out_cap"].astype(np.int64) - 61 - 128, 0).astype(np.uint64)
-    want = orc.decompress_arena(data, descs, wres, caps, codecs=(2, 3, 4))
+    want = orc.decompress_arena(data, descs, wres, caps, codecs=(1, 2, 3, 4))
     bad = np.nonzero(dres["verdict"] != want["verdicts"])[0]
     assert bad.size == 0, (f"decompress verdicts differ at {bad[:8]}: gpu {dres['verdict'][bad[:8]]} "
                            f"oracle {want['verdicts'][bad[:8]]}")
@@ -63,7 +63,7 @@ def records(rng, n, key_len, value_len, text):
     return out
 
 
-@pytest.mark.parametrize("codec", [2, 3, 4])
+@pytest.mark.parametrize("codec", [1, 2, 3, 4])
 @pytest.mark.parametrize("fmt", [WIRE, DISK])
 def test_generated_arenas(eng, codec, fmt):
     """Builder arenas (rpgen: the reference's compressor settings), text and alnum payloads."""
@@ -80,10 +80,10 @@ def test_generated_arenas(eng, codec, fmt):
 
 
 def test_mixed_codecs_corrupted(eng):
-    """C5-shaped arena: none/snappy/lz4/zstd, skewed sizes, 1-in-4 corrupted batches."""
+    """C5-shaped arena: none/gzip/snappy/lz4/zstd, skewed sizes, 1-in-4 corrupted batches."""
     from redpanda_amd import abi, engine
 
-    spec = engine.make_spec(seed=0x5EED0005, partitions=16, codec_mix=(1 << 0) | (1 << 2) | (1 << 3) | (1 << 4),
+    spec = engine.make_spec(seed=0x5EED0005, partitions=16, codec_mix=0x1F,
                             body_min=7, body_max=300_000, ops=abi.OPS_PRODUCE | abi.OP_DECOMP,
                             payload=abi.PAYLOAD_TEXT, corrupt_ppm=250_000, corrupt_mask=0x3FF)
     data, descs = engine.build_arena(spec, 160)
@@ -94,6 +94,7 @@ def test_mixed_codecs_corrupted(eng):
     assert (v == abi.V_OK).sum() > 10
     codec = got["dres"]["codec"]
     assert ((v == abi.V_OK) & (codec == 4)).sum() > 0
+    assert ((v == abi.V_OK) & (codec == 1)).sum() > 0
 
 
 def mutated_bodies(rng, codec, n):
@@ -116,8 +117,8 @@ def mutated_bodies(rng, codec, n):
             comp += bytes(rng.integers(0, 256, int(rng.integers(1, 9)), dtype=np.uint8))
         elif kind == 4 and codec == 3 and len(comp) > 11:
             comp = comp[:-4]  # no end mark: truncated right after the last block
-        elif kind == 4 and codec == 4:
-            comp += orc.compress(4, body[: len(body) // 2])  # a second frame
+        elif kind == 4 and codec in (1, 4):
+            comp += orc.compress(codec, body[: len(body) // 2])  # a second frame / gzip member
         elif kind == 5 and len(comp) > 20:
             k = int(rng.integers(16, len(comp)))
             comp[k] = 0xFF
@@ -125,7 +126,7 @@ def mutated_bodies(rng, codec, n):
     return out
 
 
-@pytest.mark.parametrize("codec", [2, 3, 4])
+@pytest.mark.parametrize("codec", [1, 2, 3, 4])
 @pytest.mark.parametrize("fmt", [WIRE, DISK])
 def test_mutated_payloads(eng, codec, fmt):
     rng = np.random.default_rng(100 + codec * 2 + fmt)
@@ -139,7 +140,7 @@ def test_large_bodies(eng):
     zstd frames larger than the 64 KiB staging buffer (streamed block by block)."""
     rng = np.random.default_rng(7)
     bs = []
-    for codec in (2, 3, 3, 2, 4, 4):
+    for codec in (2, 3, 3, 2, 4, 4, 1, 1):
         recs = records(rng, 900, 8, 1100, text=codec == 3)
         bs.append(batch(orc.compress(codec, b"".join(recs)), fmt=WIRE, record_count=len(recs), attrs=codec))
     data, descs = arena(bs, fmt=WIRE, ops=OPS)
@@ -149,9 +150,12 @@ def test_large_bodies(eng):
 def test_uncompress_scalar_mirror(eng):
     rng = np.random.default_rng(3)
     cases = []
-    for codec in (2, 3, 4):
+    for codec in (1, 2, 3, 4):
         for c, _ in mutated_bodies(rng, codec, 40):
             cases.append((codec, c))
+    gz = orc.compress(1, b"hello gzip " * 50)
+    cases += [(1, b""), (1, gz[:10]), (1, gz[:-8]), (1, gz[:-4]), (1, b"\x78\x9c\x03\x00\x00\x00\x00\x01"),
+              (1, b"\x78\x9c\x03\x00"), (1, b"\x1f\x8b\x08\x00"), (1, b"\x1f\x8b\x07\x00" + gz[4:])]
     cases += [(3, b""), (2, b""), (4, b""), (0, b"abc"), (3, b"\x04\x22\x4d"), (2, b"\x00"),
               (4, b"\x28\xb5\x2f\xfd"), (4, b"\x28\xb5\x2f\xfd\x00"), (4, b"\x50\x2a\x4d\x18\x00\x00\x00\x00")]
     for codec, c in cases:
@@ -240,7 +244,7 @@ def eng_default_uncompress(frame):
         return e.uncompress(4, frame, cap=16 << 20)
 
 
-@pytest.mark.parametrize("codec", [2, 3, 4])
+@pytest.mark.parametrize("codec", [1, 2, 3, 4])
 def test_mutated_payloads_many(eng, codec):
     """Differential fuzz of the wave-cooperative device decoders (rpgpu_wave.h)
     against the oracle: 600 library frames per codec, most of them mutated
