@@ -521,6 +521,56 @@ int32_t rpgpu_partition_summaries_device(rpgpu_ctx* ctx, const rpgpu_batch_desc*
                                          const rpgpu_batch_result* d_results, uint32_t n, uint32_t part_lo,
                                          uint32_t nparts, int64_t* d_out, void* hip_stream);
 
+/* ---- compaction keys -------------------------------------
+ * Which records survive self-compaction of a segment:
+ * segment::compaction_index_batch (storage/segment.cc:456-483) indexes every
+ * record of a compactible batch (not raft_configuration, archival_metadata or
+ * version_fence: segment_utils.h:198-203) under its key prefixed with the
+ * batch type (compacted_index.h:33-44; a null key is an empty one), keeping
+ * the latest offset per key (spill_key_index.cc:154-176);
+ * compaction_key_reducer / compacted_offset_list_reducer
+ * (compaction_reducers.cc:35-113) turn that into the set of offsets to keep,
+ * and copy_data_segment_reducer::filter keeps a record iff its offset is in
+ * the set (should_keep, compaction_reducers.h:130-133; a non-compactible batch
+ * whole, compaction_reducers.cc:117-123).
+ * Input: a validated and indexed arena (rpgpu_validate_device / submit, or the
+ * rewritten batches of the decompress path).  Batches with the same
+ * desc.partition form one compaction scope (a segment).  keep[j] for each of
+ * the index_cap index entries: 1 keep, 0 superseded by a later record with the
+ * same key, 2 not a record of an OK batch (slack between batch slices, failed
+ * batches).  *d_nkeys = distinct keys over all scopes.  The key map here is
+ * unbounded; the reference evicts entries past its memory budget
+ * (spill_key_index.cc:99-138), which can only keep more records.
+ * d_scratch: rpgpu_compaction_scratch_bytes(index_cap) bytes. */
+size_t rpgpu_compaction_scratch_bytes(uint64_t index_cap);
+int32_t rpgpu_compaction_keep_device(rpgpu_ctx* ctx, const uint8_t* d_data, const rpgpu_batch_desc* d_descs,
+                                     const rpgpu_batch_result* d_results, uint32_t n,
+                                     const rpgpu_record_index* d_index, uint64_t index_cap, uint8_t* d_keep,
+                                     uint64_t* d_nkeys, void* d_scratch, void* hip_stream);
+
+/* ---- batch timequery --------------------------------------
+ * storage::batch_timequery (storage/log_reader.cc:381-407) for batch `batch` of
+ * a validated and indexed arena: (base_offset, first_timestamp), or, when
+ * first_timestamp < time and the batch is uncompressed, the first record with
+ * first_timestamp + timestamp_delta >= time.  The batch is the first one a
+ * log_reader with first_timestamp = time returns (disk_log_impl.cc:1299-1319):
+ * rpgpu_segment_parse_device in reader mode with has_first_timestamp finds it.
+ * status: the batch's verdict (RPGPU_V_OK = result valid), -1 out of range. */
+typedef struct rpgpu_timequery {
+    uint32_t batch;
+    uint32_t reserved;
+    int64_t time;
+} rpgpu_timequery;        /* 16 bytes */
+typedef struct rpgpu_timequery_result {
+    int64_t offset;
+    int64_t time;
+    int32_t status;
+    uint32_t reserved;
+} rpgpu_timequery_result; /* 24 bytes */
+int32_t rpgpu_batch_timequery_device(rpgpu_ctx* ctx, const rpgpu_batch_result* d_results, uint32_t n,
+                                     const rpgpu_record_index* d_index, const rpgpu_timequery* d_queries,
+                                     uint32_t nq, rpgpu_timequery_result* d_out, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

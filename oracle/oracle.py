@@ -91,6 +91,10 @@ def lib() -> C.CDLL:
         L.orc_segment_index.argtypes = [vp, vp, vp, u32, vp, vp]
         L.orc_record_sets_reduce.argtypes = [u32, vp, vp, vp, vp, vp]
         L.orc_decompress_batches.argtypes = [vp, u32, vp, vp, u32, vp, vp, vp, vp, vp, vp, C.c_int]
+        L.orc_compaction_keep.restype = None
+        L.orc_compaction_keep.argtypes = [vp, vp, vp, u32, vp, u64, vp, C.POINTER(u64)]
+        L.orc_batch_timequery.restype = None
+        L.orc_batch_timequery.argtypes = [vp, u32, vp, vp, u32, vp]
         _L = L
     return _L
 
@@ -254,3 +258,32 @@ def segment_parse(data: np.ndarray, reads: np.ndarray):
         lib().orc_segment_parse(data.ctypes.data, reads[i:i + 1].ctypes.data, res[i:i + 1].ctypes.data,
                                 descs.ctypes.data)
     return res, descs[:ncap]
+
+
+def compaction_keep(data: np.ndarray, descs: np.ndarray, results: np.ndarray, index: np.ndarray):
+    """Which records survive self-compaction (oracle/compact.c): (keep, nkeys),
+    keep[j] per index entry: 1 keep, 0 superseded, 2 not a record of an OK batch."""
+    from redpanda_amd.abi import INDEX_DTYPE
+
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    descs = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+    results = np.ascontiguousarray(results, dtype=RESULT_DTYPE)
+    index = np.ascontiguousarray(index, dtype=INDEX_DTYPE)
+    keep = np.zeros(max(len(index), 1), dtype=np.uint8)
+    nkeys = C.c_uint64()
+    lib().orc_compaction_keep(data.ctypes.data, descs.ctypes.data, results.ctypes.data, len(descs),
+                              index.ctypes.data, len(index), keep.ctypes.data, C.byref(nkeys))
+    return keep[: len(index)], nkeys.value
+
+
+def batch_timequery(results: np.ndarray, index: np.ndarray, queries: np.ndarray) -> np.ndarray:
+    """storage::batch_timequery per query (oracle/compact.c)."""
+    from redpanda_amd.abi import INDEX_DTYPE, TIMEQUERY_DTYPE, TIMEQUERY_RESULT_DTYPE
+
+    results = np.ascontiguousarray(results, dtype=RESULT_DTYPE)
+    index = np.ascontiguousarray(index, dtype=INDEX_DTYPE)
+    queries = np.ascontiguousarray(queries, dtype=TIMEQUERY_DTYPE)
+    out = np.zeros(max(len(queries), 1), dtype=TIMEQUERY_RESULT_DTYPE)
+    lib().orc_batch_timequery(results.ctypes.data, len(results), index.ctypes.data, queries.ctypes.data,
+                              len(queries), out.ctypes.data)
+    return out[: len(queries)]

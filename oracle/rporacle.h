@@ -112,6 +112,14 @@ void orc_segment_index(const rpgpu_batch_desc* descs, const rpgpu_batch_result* 
 void orc_segment_parse(const uint8_t* data, const rpgpu_segment_read* rd, rpgpu_segment_parse_result* out,
                        rpgpu_batch_desc* descs);
 
+/* Compaction keys and batch timequery (compact.c): rpgpu_compaction_keep_device
+ * and rpgpu_batch_timequery_device, restated sequentially. */
+void orc_compaction_keep(const uint8_t* data, const rpgpu_batch_desc* descs, const rpgpu_batch_result* res,
+                         uint32_t n, const rpgpu_record_index* index, uint64_t index_cap, uint8_t* keep,
+                         uint64_t* nkeys);
+void orc_batch_timequery(const rpgpu_batch_result* res, uint32_t n, const rpgpu_record_index* index,
+                         const rpgpu_timequery* q, uint32_t nq, rpgpu_timequery_result* out);
+
 #ifdef __cplusplus
 }
 #endif

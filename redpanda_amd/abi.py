@@ -113,6 +113,10 @@ SEGMENT_PARSE_RESULT_DTYPE = np.dtype([("status", "<i4"), ("last_error", "<i4"),
                                        ("expected_next_batch", "<i8"), ("over_budget", "u1"), ("stopped", "u1"),
                                        ("reserved0", "<u2"), ("reserved1", "<u4")])
 assert SEGMENT_READ_DTYPE.itemsize == 112 and SEGMENT_PARSE_RESULT_DTYPE.itemsize == 64
+TIMEQUERY_DTYPE = np.dtype([("batch", "<u4"), ("reserved", "<u4"), ("time", "<i8")])
+TIMEQUERY_RESULT_DTYPE = np.dtype([("offset", "<i8"), ("time", "<i8"), ("status", "<i4"), ("reserved", "<u4")])
+assert TIMEQUERY_DTYPE.itemsize == 16 and TIMEQUERY_RESULT_DTYPE.itemsize == 24
+KEEP_DROP, KEEP_KEEP, KEEP_NONE = 0, 1, 2  # rpgpu_compaction_keep_device keep[] values
 INDEX_ENTRY_DTYPE = np.dtype([("relative_offset", "<u4"), ("relative_time", "<u4"), ("position", "<u8")])
 assert SEGMENT_DTYPE.itemsize == 32 and SEGMENT_STATE_DTYPE.itemsize == 48 and INDEX_ENTRY_DTYPE.itemsize == 16
 assert INDEX_DTYPE.itemsize == 32 and RP_HEADER_DTYPE.itemsize == 61
@@ -204,6 +208,9 @@ def lib() -> C.CDLL:
         _sig(L.rpgpu_kafka_error_codes_device, _i32, _vp, _vp, _u32, _u32, _vp, _vp)
         _sig(L.rpgpu_segment_parse_device, _i32, _vp, _vp, _vp, _u32, _vp, _vp, _vp)
         _sig(L.rpgpu_partition_summaries_device, _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
+        _sig(L.rpgpu_compaction_scratch_bytes, C.c_size_t, _u64)
+        _sig(L.rpgpu_compaction_keep_device, _i32, _vp, _vp, _vp, _vp, _u32, _vp, _u64, _vp, _vp, _vp, _vp)
+        _sig(L.rpgpu_batch_timequery_device, _i32, _vp, _vp, _u32, _vp, _vp, _u32, _vp, _vp)
         if not hasattr(L, "rpgpu_decomp_scratch_bytes"):  # an older build (A/B timing runs)
             _LIB = L
             return _LIB
@@ -242,6 +249,7 @@ EXPORTED = [
     "rpgpu_arena_alloc", "rpgpu_arena_free", "rpgpu_submit", "rpgpu_poll", "rpgpu_wait",
     "rpgpu_eventfd", "rpgpu_kafka_error_code", "rpgpu_kafka_error_codes_device",
     "rpgpu_partition_summaries_device", "rpgpu_segment_parse_device",
+    "rpgpu_compaction_scratch_bytes", "rpgpu_compaction_keep_device", "rpgpu_batch_timequery_device",
     "rpgpu_validate_scratch_bytes", "rpgpu_validate_device", "rpgpu_plan_device",
     "rpgpu_run_device", "rpgpu_crc32c_ranges_device",
     "rpgpu_crc32c_extend", "rpgpu_internal_header_only_crc", "rpgpu_crc_record_batch",

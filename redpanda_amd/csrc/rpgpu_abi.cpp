@@ -69,6 +69,13 @@ hipError_t launch_segment_parse(const uint8_t* d_data, const rpgpu_segment_read*
                                 const uint32_t* d_tables, int grid, hipStream_t s);
 hipError_t launch_summaries(const rpgpu_batch_desc* d_descs, const rpgpu_batch_result* d_res, uint32_t n,
                             uint32_t part_lo, uint32_t nparts, int64_t* d_out, hipStream_t s);
+size_t compaction_scratch_bytes(uint64_t index_cap);
+hipError_t launch_compaction_keep(const uint8_t* d_data, const rpgpu_batch_desc* d_descs,
+                                  const rpgpu_batch_result* d_res, uint32_t n, const rpgpu_record_index* d_index,
+                                  uint64_t index_cap, uint8_t* d_keep, uint64_t* d_nkeys, void* d_scratch,
+                                  hipStream_t s);
+hipError_t launch_timequery(const rpgpu_batch_result* d_res, uint32_t n, const rpgpu_record_index* d_index,
+                            const rpgpu_timequery* d_q, uint32_t nq, rpgpu_timequery_result* d_out, hipStream_t s);
 }  // namespace rpgpu
 
 namespace {
@@ -269,6 +276,32 @@ int32_t rpgpu_partition_summaries_device(rpgpu_ctx* c, const rpgpu_batch_desc* d
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     hipError_t e = rpgpu::launch_summaries(d_descs, d_results, n, part_lo, nparts, d_out, s);
     if (e != hipSuccess) return fail(c, e, "summaries launch");
+    return RPGPU_OK;
+}
+
+size_t rpgpu_compaction_scratch_bytes(uint64_t index_cap) { return rpgpu::compaction_scratch_bytes(index_cap); }
+
+int32_t rpgpu_compaction_keep_device(rpgpu_ctx* c, const uint8_t* d_data, const rpgpu_batch_desc* d_descs,
+                                     const rpgpu_batch_result* d_results, uint32_t n,
+                                     const rpgpu_record_index* d_index, uint64_t index_cap, uint8_t* d_keep,
+                                     uint64_t* d_nkeys, void* d_scratch, void* hip_stream) {
+    if (!c || !d_nkeys || (n && (!d_data || !d_descs || !d_results)) ||
+        (index_cap && (!d_index || !d_keep || !d_scratch)) || index_cap > 0xffffffffull)
+        return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_compaction_keep(d_data, d_descs, d_results, n, d_index, index_cap, d_keep, d_nkeys,
+                                                 d_scratch, s);
+    if (e != hipSuccess) return fail(c, e, "compaction launch");
+    return RPGPU_OK;
+}
+
+int32_t rpgpu_batch_timequery_device(rpgpu_ctx* c, const rpgpu_batch_result* d_results, uint32_t n,
+                                     const rpgpu_record_index* d_index, const rpgpu_timequery* d_queries,
+                                     uint32_t nq, rpgpu_timequery_result* d_out, void* hip_stream) {
+    if (!c || (nq && (!d_queries || !d_out || (n && (!d_results || !d_index))))) return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_timequery(d_results, n, d_index, d_queries, nq, d_out, s);
+    if (e != hipSuccess) return fail(c, e, "timequery launch");
     return RPGPU_OK;
 }
 

@@ -294,6 +294,77 @@ class Engine:
         return dict(results=d_res.cpu().numpy().view(abi.SEGMENT_PARSE_RESULT_DTYPE)[:n].copy(),
                     descs=d_descs.cpu().numpy().view(abi.DESC_DTYPE)[:ncap].copy())
 
+    def compaction_keep(self, data: np.ndarray, descs: np.ndarray, results: np.ndarray,
+                        index: np.ndarray) -> tuple[np.ndarray, int]:
+        """rpgpu_compaction_keep_device over a validated + indexed arena (host
+        copies in, host copies out): (keep per index entry, distinct keys)."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        sh = torch.cuda.current_stream(dev).cuda_stream
+        n, cap = len(descs), len(index)
+
+        def up(a, dtype):
+            a = np.ascontiguousarray(a, dtype=dtype)
+            return torch.from_numpy(a.view(np.uint8).reshape(-1).copy()).to(dev)
+
+        d_data = up(np.concatenate([np.asarray(data, np.uint8), np.zeros(abi.ARENA_TAIL_PAD, np.uint8)]), np.uint8)
+        d_descs, d_res, d_idx = up(descs, abi.DESC_DTYPE), up(results, abi.RESULT_DTYPE), up(index, abi.INDEX_DTYPE)
+        d_keep = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+        d_nkeys = torch.empty(1, dtype=torch.int64, device=dev)
+        d_scr = torch.empty(max(int(self._lib.rpgpu_compaction_scratch_bytes(cap)), 1), dtype=torch.uint8, device=dev)
+        rc = self._lib.rpgpu_compaction_keep_device(self._ctx, d_data.data_ptr(), d_descs.data_ptr(), d_res.data_ptr(),
+                                                    n, d_idx.data_ptr(), cap, d_keep.data_ptr(), d_nkeys.data_ptr(),
+                                                    d_scr.data_ptr(), sh)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_compaction_keep_device: {rc} {self.last_error()}")
+        torch.cuda.synchronize(dev)
+        return d_keep.cpu().numpy()[:cap].copy(), int(d_nkeys.item())
+
+    def batch_timequery(self, results: np.ndarray, index: np.ndarray, queries: np.ndarray) -> np.ndarray:
+        """rpgpu_batch_timequery_device (storage::batch_timequery) per query."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        sh = torch.cuda.current_stream(dev).cuda_stream
+        results = np.ascontiguousarray(results, dtype=abi.RESULT_DTYPE)
+        index = np.ascontiguousarray(index, dtype=abi.INDEX_DTYPE)
+        queries = np.ascontiguousarray(queries, dtype=abi.TIMEQUERY_DTYPE)
+        nq = len(queries)
+
+        def up(a):
+            return torch.from_numpy(a.view(np.uint8).reshape(-1).copy() if a.size else np.zeros(64, np.uint8)).to(dev)
+
+        d_res, d_idx, d_q = up(results), up(index), up(queries)
+        d_out = torch.zeros(max(nq, 1) * abi.TIMEQUERY_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        rc = self._lib.rpgpu_batch_timequery_device(self._ctx, d_res.data_ptr(), len(results), d_idx.data_ptr(),
+                                                    d_q.data_ptr(), nq, d_out.data_ptr(), sh)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_batch_timequery_device: {rc} {self.last_error()}")
+        torch.cuda.synchronize(dev)
+        return d_out.cpu().numpy().view(abi.TIMEQUERY_RESULT_DTYPE)[:nq].copy()
+
+    def timequery(self, data: np.ndarray, read: np.ndarray):
+        """disk_log_impl::timequery (storage/disk_log_impl.cc:1299-1319) over one
+        segment on the GPU: the reader (rpgpu_segment_parse_device, reader mode,
+        first_timestamp = the query time) picks the first batch, which is
+        validated and indexed, and batch_timequery runs on it if its
+        max_timestamp >= time.  Returns (offset, time) or None."""
+        read = np.ascontiguousarray(read, dtype=abi.SEGMENT_READ_DTYPE).reshape(1)
+        parsed = self.segment_parse(data, read)
+        if parsed["results"]["accepted"][0] == 0:
+            return None
+        d = parsed["descs"][int(read["desc_first"][0]): int(read["desc_first"][0]) + 1].copy()
+        d["ops"] = abi.OP_PARSE | abi.OP_INDEX  # the header CRC was checked by the parser
+        res, idx, _ = self.submit(data, d)
+        t = int(read["first_timestamp"][0])
+        if res["verdict"][0] != abi.V_OK or res["max_timestamp"][0] < t:
+            return None
+        q = np.zeros(1, dtype=abi.TIMEQUERY_DTYPE)
+        q["time"] = t
+        o = self.batch_timequery(res, idx, q)[0]
+        return int(o["offset"]), int(o["time"])
+
     # -- synchronous scalar mirrors ---------------------------------------------------
     def uncompress(self, codec: int, data: bytes | np.ndarray, cap: int | None = None) -> tuple[int, bytes]:
         """compression::compressor::uncompress on the GPU: (verdict, bytes)."""
