@@ -548,6 +548,49 @@ int32_t rpgpu_compaction_keep_device(rpgpu_ctx* ctx, const uint8_t* d_data, cons
                                      const rpgpu_record_index* d_index, uint64_t index_cap, uint8_t* d_keep,
                                      uint64_t* d_nkeys, void* d_scratch, void* hip_stream);
 
+/* ---- fetch serialization ----------------------------------
+ * kafka_batch_serializer (kafka/protocol/batch_consumer.h:26-101) over batches a
+ * reader returns: each on-disk batch becomes a Kafka v2 wire batch,
+ * writer_serialize_batch (kafka/protocol/wire.h:645-681) -- big-endian
+ * header, batch_length = size_bytes - 12, partition leader epoch =
+ * leader_epoch_from_term(term) (kafka/types.h:117-124: -1 when the term does
+ * not fit int32), magic 2, the stored Kafka crc, then the records bytes
+ * unchanged.  A wire batch is exactly as long as the on-disk one, so batch i
+ * is written at d_out + d_descs[i].offset: d_out mirrors the arena and a
+ * contiguous run of batches stays contiguous (d_out must not overlap
+ * d_data).  d_terms: the term of each
+ * batch (record_batch::term(), set by the reader from its segment), or NULL
+ * for term 0.  The header is read from the batch bytes (format must be
+ * RPGPU_FMT_RP_DISK; size_bytes < 61 or > desc.length writes nothing and
+ * counts as an error in the range's status).
+ * Optional per-range summaries (the serializer's result, :29-40, built by
+ * operator() and end_of_stream, :54-77): for the
+ * batches [first, first + count) of d_descs, in order: record_count (uint32
+ * sum), base_offset (of the batch at which the running record count was 0),
+ * last_offset, first_tx_batch_offset (INT64_MIN with has_first_tx = 0 when
+ * no batch is transactional), output bytes.  Empty range: offsets INT64_MIN
+ * (a default model::offset). */
+typedef struct rpgpu_fetch_range {
+    uint32_t first;
+    uint32_t count;
+} rpgpu_fetch_range;      /* 8 bytes */
+typedef struct rpgpu_fetch_summary {
+    int64_t base_offset;
+    int64_t last_offset;
+    int64_t first_tx_batch_offset;
+    uint64_t bytes;
+    uint32_t record_count;
+    uint8_t has_first_tx;
+    uint8_t reserved0;
+    uint16_t reserved1;
+    int32_t status;       /* 0, or the number of batches with a bad size */
+    uint32_t reserved2;
+} rpgpu_fetch_summary;    /* 48 bytes */
+int32_t rpgpu_kafka_serialize_device(rpgpu_ctx* ctx, const uint8_t* d_data, const rpgpu_batch_desc* d_descs,
+                                     const int64_t* d_terms, uint32_t n, uint8_t* d_out,
+                                     const rpgpu_fetch_range* d_ranges, uint32_t nranges,
+                                     rpgpu_fetch_summary* d_summaries, void* hip_stream);
+
 /* ---- batch timequery --------------------------------------
  * storage::batch_timequery (storage/log_reader.cc:381-407) for batch `batch` of
  * a validated and indexed arena: (base_offset, first_timestamp), or, when

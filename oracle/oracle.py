@@ -95,6 +95,8 @@ def lib() -> C.CDLL:
         L.orc_compaction_keep.argtypes = [vp, vp, vp, u32, vp, u64, vp, C.POINTER(u64)]
         L.orc_batch_timequery.restype = None
         L.orc_batch_timequery.argtypes = [vp, u32, vp, vp, u32, vp]
+        L.orc_kafka_serialize.restype = None
+        L.orc_kafka_serialize.argtypes = [vp, vp, vp, u32, vp, vp, u32, vp]
         _L = L
     return _L
 
@@ -287,3 +289,18 @@ def batch_timequery(results: np.ndarray, index: np.ndarray, queries: np.ndarray)
     lib().orc_batch_timequery(results.ctypes.data, len(results), index.ctypes.data, queries.ctypes.data,
                               len(queries), out.ctypes.data)
     return out[: len(queries)]
+
+
+def kafka_serialize(data: np.ndarray, descs: np.ndarray, terms=None, ranges=None):
+    """kafka_batch_serializer over on-disk batches (oracle/fetch.c): (out, summaries)."""
+    from redpanda_amd.abi import FETCH_RANGE_DTYPE, FETCH_SUMMARY_DTYPE
+
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    descs = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+    out = np.zeros_like(data)
+    t = None if terms is None else np.ascontiguousarray(terms, dtype=np.int64)
+    rg = np.zeros(0, dtype=FETCH_RANGE_DTYPE) if ranges is None else np.ascontiguousarray(ranges, FETCH_RANGE_DTYPE)
+    sums = np.zeros(max(len(rg), 1), dtype=FETCH_SUMMARY_DTYPE)
+    lib().orc_kafka_serialize(data.ctypes.data, descs.ctypes.data, None if t is None else t.ctypes.data, len(descs),
+                              out.ctypes.data, rg.ctypes.data, len(rg), sums.ctypes.data)
+    return out, sums[: len(rg)]

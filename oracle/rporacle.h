@@ -120,6 +120,10 @@ void orc_compaction_keep(const uint8_t* data, const rpgpu_batch_desc* descs, con
 void orc_batch_timequery(const rpgpu_batch_result* res, uint32_t n, const rpgpu_record_index* index,
                          const rpgpu_timequery* q, uint32_t nq, rpgpu_timequery_result* out);
 
+/* Fetch serialization (fetch.c): rpgpu_kafka_serialize_device restated. */
+void orc_kafka_serialize(const uint8_t* data, const rpgpu_batch_desc* descs, const int64_t* terms, uint32_t n,
+                         uint8_t* out, const rpgpu_fetch_range* ranges, uint32_t nranges, rpgpu_fetch_summary* sums);
+
 #ifdef __cplusplus
 }
 #endif

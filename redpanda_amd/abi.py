@@ -116,7 +116,12 @@ assert SEGMENT_READ_DTYPE.itemsize == 112 and SEGMENT_PARSE_RESULT_DTYPE.itemsiz
 TIMEQUERY_DTYPE = np.dtype([("batch", "<u4"), ("reserved", "<u4"), ("time", "<i8")])
 TIMEQUERY_RESULT_DTYPE = np.dtype([("offset", "<i8"), ("time", "<i8"), ("status", "<i4"), ("reserved", "<u4")])
 assert TIMEQUERY_DTYPE.itemsize == 16 and TIMEQUERY_RESULT_DTYPE.itemsize == 24
-KEEP_DROP, KEEP_KEEP, KEEP_NONE = 0, 1, 2  # rpgpu_compaction_keep_device keep[] values
+KEEP_DROP, KEEP_KEEP, KEEP_NONE = 0, 1, 2
+FETCH_RANGE_DTYPE = np.dtype([("first", "<u4"), ("count", "<u4")])
+FETCH_SUMMARY_DTYPE = np.dtype([("base_offset", "<i8"), ("last_offset", "<i8"), ("first_tx_batch_offset", "<i8"),
+                                ("bytes", "<u8"), ("record_count", "<u4"), ("has_first_tx", "u1"),
+                                ("reserved0", "u1"), ("reserved1", "<u2"), ("status", "<i4"), ("reserved2", "<u4")])
+assert FETCH_SUMMARY_DTYPE.itemsize == 48  # rpgpu_compaction_keep_device keep[] values
 INDEX_ENTRY_DTYPE = np.dtype([("relative_offset", "<u4"), ("relative_time", "<u4"), ("position", "<u8")])
 assert SEGMENT_DTYPE.itemsize == 32 and SEGMENT_STATE_DTYPE.itemsize == 48 and INDEX_ENTRY_DTYPE.itemsize == 16
 assert INDEX_DTYPE.itemsize == 32 and RP_HEADER_DTYPE.itemsize == 61
@@ -211,6 +216,7 @@ def lib() -> C.CDLL:
         _sig(L.rpgpu_compaction_scratch_bytes, C.c_size_t, _u64)
         _sig(L.rpgpu_compaction_keep_device, _i32, _vp, _vp, _vp, _vp, _u32, _vp, _u64, _vp, _vp, _vp, _vp)
         _sig(L.rpgpu_batch_timequery_device, _i32, _vp, _vp, _u32, _vp, _vp, _u32, _vp, _vp)
+        _sig(L.rpgpu_kafka_serialize_device, _i32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _u32, _vp, _vp)
         if not hasattr(L, "rpgpu_decomp_scratch_bytes"):  # an older build (A/B timing runs)
             _LIB = L
             return _LIB
@@ -250,6 +256,7 @@ EXPORTED = [
     "rpgpu_eventfd", "rpgpu_kafka_error_code", "rpgpu_kafka_error_codes_device",
     "rpgpu_partition_summaries_device", "rpgpu_segment_parse_device",
     "rpgpu_compaction_scratch_bytes", "rpgpu_compaction_keep_device", "rpgpu_batch_timequery_device",
+    "rpgpu_kafka_serialize_device",
     "rpgpu_validate_scratch_bytes", "rpgpu_validate_device", "rpgpu_plan_device",
     "rpgpu_run_device", "rpgpu_crc32c_ranges_device",
     "rpgpu_crc32c_extend", "rpgpu_internal_header_only_crc", "rpgpu_crc_record_batch",

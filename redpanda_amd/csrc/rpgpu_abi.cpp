@@ -76,6 +76,9 @@ hipError_t launch_compaction_keep(const uint8_t* d_data, const rpgpu_batch_desc*
                                   hipStream_t s);
 hipError_t launch_timequery(const rpgpu_batch_result* d_res, uint32_t n, const rpgpu_record_index* d_index,
                             const rpgpu_timequery* d_q, uint32_t nq, rpgpu_timequery_result* d_out, hipStream_t s);
+hipError_t launch_kafka_serialize(const uint8_t* d_data, const rpgpu_batch_desc* d_descs, const int64_t* d_terms,
+                                  uint32_t n, uint8_t* d_out, const rpgpu_fetch_range* d_ranges, uint32_t nranges,
+                                  rpgpu_fetch_summary* d_sums, hipStream_t s);
 }  // namespace rpgpu
 
 namespace {
@@ -292,6 +295,19 @@ int32_t rpgpu_compaction_keep_device(rpgpu_ctx* c, const uint8_t* d_data, const 
     hipError_t e = rpgpu::launch_compaction_keep(d_data, d_descs, d_results, n, d_index, index_cap, d_keep, d_nkeys,
                                                  d_scratch, s);
     if (e != hipSuccess) return fail(c, e, "compaction launch");
+    return RPGPU_OK;
+}
+
+int32_t rpgpu_kafka_serialize_device(rpgpu_ctx* c, const uint8_t* d_data, const rpgpu_batch_desc* d_descs,
+                                     const int64_t* d_terms, uint32_t n, uint8_t* d_out,
+                                     const rpgpu_fetch_range* d_ranges, uint32_t nranges,
+                                     rpgpu_fetch_summary* d_summaries, void* hip_stream) {
+    if (!c || (n && (!d_data || !d_descs || !d_out)) || (nranges && (!d_ranges || !d_summaries)) ||
+        (n && d_data == d_out))
+        return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_kafka_serialize(d_data, d_descs, d_terms, n, d_out, d_ranges, nranges, d_summaries, s);
+    if (e != hipSuccess) return fail(c, e, "serialize launch");
     return RPGPU_OK;
 }
 

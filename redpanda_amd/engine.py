@@ -321,6 +321,35 @@ class Engine:
         torch.cuda.synchronize(dev)
         return d_keep.cpu().numpy()[:cap].copy(), int(d_nkeys.item())
 
+    def kafka_serialize(self, data: np.ndarray, descs: np.ndarray, terms=None, ranges=None):
+        """rpgpu_kafka_serialize_device: on-disk batches -> Kafka wire batches at
+        the same offsets, plus per-range serializer summaries.  (out, summaries)."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        sh = torch.cuda.current_stream(dev).cuda_stream
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        descs = np.ascontiguousarray(descs, dtype=abi.DESC_DTYPE)
+        rg = np.zeros(0, dtype=abi.FETCH_RANGE_DTYPE) if ranges is None else \
+            np.ascontiguousarray(ranges, dtype=abi.FETCH_RANGE_DTYPE)
+        n, nr = len(descs), len(rg)
+        d_data = torch.from_numpy(np.concatenate([data, np.zeros(abi.ARENA_TAIL_PAD, np.uint8)])).to(dev)
+        d_out = torch.zeros_like(d_data)
+        d_descs = torch.from_numpy(descs.view(np.uint8).copy() if n else np.zeros(24, np.uint8)).to(dev)
+        d_terms = None
+        if terms is not None:
+            d_terms = torch.from_numpy(np.ascontiguousarray(terms, dtype=np.int64).copy()).to(dev)
+        d_rg = torch.from_numpy(rg.view(np.uint8).copy() if nr else np.zeros(8, np.uint8)).to(dev)
+        d_sums = torch.zeros(max(nr, 1) * abi.FETCH_SUMMARY_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        rc = self._lib.rpgpu_kafka_serialize_device(self._ctx, d_data.data_ptr(), d_descs.data_ptr(),
+                                                    d_terms.data_ptr() if d_terms is not None else None, n,
+                                                    d_out.data_ptr(), d_rg.data_ptr(), nr, d_sums.data_ptr(), sh)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_kafka_serialize_device: {rc} {self.last_error()}")
+        torch.cuda.synchronize(dev)
+        return (d_out.cpu().numpy()[: data.size].copy(),
+                d_sums.cpu().numpy().view(abi.FETCH_SUMMARY_DTYPE)[:nr].copy())
+
     def batch_timequery(self, results: np.ndarray, index: np.ndarray, queries: np.ndarray) -> np.ndarray:
         """rpgpu_batch_timequery_device (storage::batch_timequery) per query."""
         import torch
