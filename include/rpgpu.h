@@ -356,6 +356,31 @@ int32_t rpgpu_decomp_run_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_descs,
                                 rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_out_results,
                                 rpgpu_record_index* d_index, uint64_t index_cap,
                                 uint64_t* d_index_used, void* d_scratch, void* hip_stream);
+
+/* ---- compression (the encode side) -------------------------
+ * storage::internal::compress_batch (storage/parser_utils.cc:89-119) for every
+ * batch of a validated arena that is OK and uncompressed: the records bytes
+ * through compression::compressor::compress (compression/compression.cc:
+ * 19-35) -- codec 3, LZ4 frame (lz4_frame_compressor.cc:68-158), and codec 2,
+ * snappy-java (snappy_java_compressor.cc:58-75), byte-identical to liblz4
+ * 1.9.3 / snappy 1.1.8 through the reference's loops (a body is one iobuf
+ * fragment per 128 KiB) -- and a rewritten on-disk batch: attrs |= codec,
+ * size_bytes = 61 + payload, fresh crc and header_crc
+ * (reset_size_checksum_metadata, :122-128).  Same two-call shape as the
+ * decompress path: plan (output slot per batch = header + the codec's bound,
+ * total in *d_out_bytes), then run.  d_cres[i] (an rpgpu_decomp_result):
+ * verdict OK / SKIPPED (not OK or already compressed) / DECOMP_OVERFLOW
+ * (out_cap below the plan), out_offset, out_len (payload bytes), out_cap;
+ * d_out_descs / d_out_results: the compressed batches and their validation
+ * (crc, header_crc).  Other codecs: RPGPU_EINVAL. */
+size_t rpgpu_compress_scratch_bytes(uint32_t n);
+int32_t rpgpu_compress_plan_device(rpgpu_ctx* ctx, const rpgpu_batch_result* d_results, uint32_t n, int32_t codec,
+                                   uint64_t* d_out_bytes, void* d_scratch, void* hip_stream);
+int32_t rpgpu_compress_run_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_descs, uint32_t n,
+                                  const uint8_t* d_data, const rpgpu_batch_result* d_results, int32_t codec,
+                                  rpgpu_decomp_result* d_cres, uint8_t* d_out, uint64_t out_cap,
+                                  rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_out_results,
+                                  void* d_scratch, void* hip_stream);
 /* Synchronous scalar mirror of compression::compressor::uncompress(buf, codec)
  * on the GPU, host buffers.  Returns the verdict (>= 0) or a negative status;
  * *out_len = decompressed bytes (the size needed when the verdict is

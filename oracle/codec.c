@@ -279,14 +279,33 @@ int32_t orc_compress(int codec, const uint8_t* in, size_t n, uint8_t* out, size_
                      size_t* out_len) {
     switch (codec) {
     case 3: {
+        /* lz4_frame_compressor::compress (lz4_frame_compressor.cc:68-158):
+         * LZ4F_compressBegin, LZ4F_compressUpdate over input chunks of at most
+         * max_chunk_size / 2 = 64 KiB (one iobuf fragment: the whole body),
+         * LZ4F_compressEnd.  The reference's output-buffer switching moves
+         * where the bytes land in the iobuf, not the bytes. */
         LZ4F_preferences_t prefs;
         memset(&prefs, 0, sizeof(prefs));
         prefs.compressionLevel = 1;
         prefs.frameInfo.blockMode = LZ4F_blockIndependent;
         prefs.frameInfo.contentSize = n;
-        size_t r = LZ4F_compressFrame(out, cap, in, n, &prefs);
+        LZ4F_cctx* cx = NULL;
+        if (LZ4F_isError(LZ4F_createCompressionContext(&cx, LZ4F_VERSION))) return RPGPU_V_DECOMP_ERROR;
+        size_t o = LZ4F_compressBegin(cx, out, cap, &prefs);
+        size_t r = o;
+        for (size_t i = 0; !LZ4F_isError(r) && i < n;) {
+            const size_t m = n - i < MAX_CHUNK / 2 ? n - i : MAX_CHUNK / 2;
+            r = LZ4F_compressUpdate(cx, out + o, cap - o, in + i, m, NULL);
+            if (!LZ4F_isError(r)) o += r;
+            i += m;
+        }
+        if (!LZ4F_isError(r)) {
+            r = LZ4F_compressEnd(cx, out + o, cap - o, NULL);
+            if (!LZ4F_isError(r)) o += r;
+        }
+        LZ4F_freeCompressionContext(cx);
         if (LZ4F_isError(r)) return RPGPU_V_DECOMP_ERROR;
-        *out_len = r;
+        *out_len = o;
         return RPGPU_V_OK;
     }
     case 4: {

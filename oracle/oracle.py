@@ -304,3 +304,36 @@ def kafka_serialize(data: np.ndarray, descs: np.ndarray, terms=None, ranges=None
     lib().orc_kafka_serialize(data.ctypes.data, descs.ctypes.data, None if t is None else t.ctypes.data, len(descs),
                               out.ctypes.data, rg.ctypes.data, len(rg), sums.ctypes.data)
     return out, sums[: len(rg)]
+
+
+def compress_batches(data: np.ndarray, descs: np.ndarray, results: np.ndarray, codec: int) -> list:
+    """storage::internal::compress_batch (storage/parser_utils.cc:89-128) per
+    batch that validated OK and is uncompressed: the compressed on-disk batch
+    bytes (attrs |= codec, size_bytes, crc, header_crc reset), else None.  The
+    payload is compressor::compress through the reference's loops (compress())."""
+    import struct
+
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    out = []
+    for i in range(len(descs)):
+        r = results[i]
+        if int(r["verdict"]) != 0 or int(r["codec"]) != 0:
+            out.append(None)
+            continue
+        o = int(descs["offset"][i])
+        wire = int(descs["format"][i]) == 0
+        raw = data[o:o + int(r["size_bytes"])].tobytes()
+        payload = compress(codec, raw[61:])
+        h = np.zeros(1, dtype=RP_HEADER_DTYPE)
+        fmt = ">" if wire else "<"
+        h["size_bytes"] = 61 + len(payload)
+        h["base_offset"] = struct.unpack_from(fmt + "q", raw, 0 if wire else 8)[0]
+        h["type"] = 1 if wire else struct.unpack_from("b", raw, 16)[0]
+        attrs, lod, fts, mts, pid, pep, bseq, rc = struct.unpack_from(fmt + "hiqqqhii", raw, 21)
+        h["attrs"] = (attrs & ~7) | codec
+        h["last_offset_delta"], h["first_timestamp"], h["max_timestamp"] = lod, fts, mts
+        h["producer_id"], h["producer_epoch"], h["base_sequence"], h["record_count"] = pid, pep, bseq, rc
+        h["crc"] = crc_record_batch(h, payload)
+        h["header_crc"] = internal_header_only_crc(h)
+        out.append(h.tobytes() + payload)
+    return out

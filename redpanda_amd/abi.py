@@ -217,6 +217,9 @@ def lib() -> C.CDLL:
         _sig(L.rpgpu_compaction_keep_device, _i32, _vp, _vp, _vp, _vp, _u32, _vp, _u64, _vp, _vp, _vp, _vp)
         _sig(L.rpgpu_batch_timequery_device, _i32, _vp, _vp, _u32, _vp, _vp, _u32, _vp, _vp)
         _sig(L.rpgpu_kafka_serialize_device, _i32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _u32, _vp, _vp)
+        _sig(L.rpgpu_compress_scratch_bytes, C.c_size_t, _u32)
+        _sig(L.rpgpu_compress_plan_device, _i32, _vp, _vp, _u32, _i32, _vp, _vp, _vp)
+        _sig(L.rpgpu_compress_run_device, _i32, _vp, _vp, _u32, _vp, _vp, _i32, _vp, _vp, _u64, _vp, _vp, _vp, _vp)
         if not hasattr(L, "rpgpu_decomp_scratch_bytes"):  # an older build (A/B timing runs)
             _LIB = L
             return _LIB
@@ -256,7 +259,8 @@ EXPORTED = [
     "rpgpu_eventfd", "rpgpu_kafka_error_code", "rpgpu_kafka_error_codes_device",
     "rpgpu_partition_summaries_device", "rpgpu_segment_parse_device",
     "rpgpu_compaction_scratch_bytes", "rpgpu_compaction_keep_device", "rpgpu_batch_timequery_device",
-    "rpgpu_kafka_serialize_device",
+    "rpgpu_kafka_serialize_device", "rpgpu_compress_scratch_bytes", "rpgpu_compress_plan_device",
+    "rpgpu_compress_run_device",
     "rpgpu_validate_scratch_bytes", "rpgpu_validate_device", "rpgpu_plan_device",
     "rpgpu_run_device", "rpgpu_crc32c_ranges_device",
     "rpgpu_crc32c_extend", "rpgpu_internal_header_only_crc", "rpgpu_crc_record_batch",

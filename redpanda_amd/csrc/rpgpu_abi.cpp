@@ -76,6 +76,14 @@ hipError_t launch_compaction_keep(const uint8_t* d_data, const rpgpu_batch_desc*
                                   hipStream_t s);
 hipError_t launch_timequery(const rpgpu_batch_result* d_res, uint32_t n, const rpgpu_record_index* d_index,
                             const rpgpu_timequery* d_q, uint32_t nq, rpgpu_timequery_result* d_out, hipStream_t s);
+size_t compress_scratch_bytes(uint32_t n);
+hipError_t launch_compress_plan(const rpgpu_batch_result* d_vres, uint32_t n, uint32_t codec, uint64_t* d_out_bytes,
+                                void* d_scratch, hipStream_t s);
+hipError_t launch_compress_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
+                               const rpgpu_batch_result* d_vres, uint32_t codec, rpgpu_decomp_result* d_cres,
+                               uint8_t* d_out, uint64_t out_cap, rpgpu_batch_desc* d_out_descs,
+                               rpgpu_batch_result* d_vres2, void* d_scratch, const uint32_t* d_tables, int grid,
+                               hipStream_t s);
 hipError_t launch_kafka_serialize(const uint8_t* d_data, const rpgpu_batch_desc* d_descs, const int64_t* d_terms,
                                   uint32_t n, uint8_t* d_out, const rpgpu_fetch_range* d_ranges, uint32_t nranges,
                                   rpgpu_fetch_summary* d_sums, hipStream_t s);
@@ -417,6 +425,33 @@ int32_t rpgpu_decomp_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, u
                                             c->have_overlap ? &c->overlap : nullptr,
                                             c->have_dstreams ? &c->dstreams : nullptr);
     if (e != hipSuccess) return fail(c, e, "decomp run launch");
+    return RPGPU_OK;
+}
+
+size_t rpgpu_compress_scratch_bytes(uint32_t n) { return rpgpu::compress_scratch_bytes(n); }
+
+int32_t rpgpu_compress_plan_device(rpgpu_ctx* c, const rpgpu_batch_result* d_results, uint32_t n, int32_t codec,
+                                   uint64_t* d_out_bytes, void* d_scratch, void* hip_stream) {
+    if (!c || (codec != 2 && codec != 3) || (n && (!d_results || !d_scratch))) return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_compress_plan(d_results, n, (uint32_t)codec, d_out_bytes, d_scratch, s);
+    if (e != hipSuccess) return fail(c, e, "compress plan launch");
+    return RPGPU_OK;
+}
+
+int32_t rpgpu_compress_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, uint32_t n,
+                                  const uint8_t* d_data, const rpgpu_batch_result* d_results, int32_t codec,
+                                  rpgpu_decomp_result* d_cres, uint8_t* d_out, uint64_t out_cap,
+                                  rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_out_results,
+                                  void* d_scratch, void* hip_stream) {
+    if (!c || (codec != 2 && codec != 3) ||
+        (n && (!d_descs || !d_data || !d_results || !d_cres || !d_out || !d_out_descs || !d_out_results ||
+               !d_scratch)))
+        return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_compress_run(d_descs, n, d_data, d_results, (uint32_t)codec, d_cres, d_out, out_cap,
+                                              d_out_descs, d_out_results, d_scratch, c->d_tables, c->grid, s);
+    if (e != hipSuccess) return fail(c, e, "compress run launch");
     return RPGPU_OK;
 }
 

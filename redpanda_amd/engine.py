@@ -194,6 +194,53 @@ class Engine:
             index=d_index.cpu().numpy().view(abi.INDEX_DTYPE)[: min(used, index_cap)].copy(),
             used=used, out_bytes=out_bytes)
 
+    def compress_arena(self, data: np.ndarray, descs: np.ndarray, codec: int) -> dict:
+        """Validate a host arena, then compress its OK uncompressed batches
+        (rpgpu_compress_plan_device / rpgpu_compress_run_device).  Returns host
+        copies: results, cres, out, out_descs, out_results, out_bytes."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        descs = np.ascontiguousarray(descs, dtype=abi.DESC_DTYPE)
+        n = len(descs)
+        sh = torch.cuda.current_stream(dev).cuda_stream
+        m = max(n, 1)
+        d_data = torch.from_numpy(data.copy()).to(dev)
+        d_descs = torch.from_numpy(descs.view(np.uint8).copy()).to(dev)
+        d_res = torch.zeros(m * 64, dtype=torch.uint8, device=dev)
+        d_used = torch.zeros(2, dtype=torch.int64, device=dev)
+        d_vscr = torch.zeros(max(self.scratch_bytes(n), 1), dtype=torch.uint8, device=dev)
+        index0_cap = int(descs["length"].astype(np.uint64).sum() // 2) + 1
+        d_index0 = torch.zeros(index0_cap * 32, dtype=torch.uint8, device=dev)
+        self.validate_device(d_descs.data_ptr(), n, d_data.data_ptr(), d_res.data_ptr(),
+                             d_index0.data_ptr(), index0_cap, d_used.data_ptr(), d_vscr.data_ptr(), sh)
+        d_scr = torch.empty(max(int(self._lib.rpgpu_compress_scratch_bytes(n)), 1), dtype=torch.uint8, device=dev)
+        rc = self._lib.rpgpu_compress_plan_device(self._ctx, d_res.data_ptr(), n, codec, d_used.data_ptr(),
+                                                  d_scr.data_ptr(), sh)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_compress_plan_device: {rc} {self.last_error()}")
+        torch.cuda.synchronize(dev)
+        out_bytes = int(d_used[0].item())
+        out_cap = out_bytes + abi.ARENA_TAIL_PAD
+        d_out = torch.zeros(out_cap, dtype=torch.uint8, device=dev)
+        d_cres = torch.zeros(m * 32, dtype=torch.uint8, device=dev)
+        d_odescs = torch.zeros(m * 24, dtype=torch.uint8, device=dev)
+        d_ores = torch.zeros(m * 64, dtype=torch.uint8, device=dev)
+        rc = self._lib.rpgpu_compress_run_device(self._ctx, d_descs.data_ptr(), n, d_data.data_ptr(), d_res.data_ptr(),
+                                                 codec, d_cres.data_ptr(), d_out.data_ptr(), out_cap,
+                                                 d_odescs.data_ptr(), d_ores.data_ptr(), d_scr.data_ptr(), sh)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_compress_run_device: {rc} {self.last_error()}")
+        torch.cuda.synchronize(dev)
+        return dict(
+            results=d_res.cpu().numpy().view(abi.RESULT_DTYPE)[:n].copy(),
+            cres=d_cres.cpu().numpy().view(abi.DECOMP_RESULT_DTYPE)[:n].copy(),
+            out=d_out.cpu().numpy(),
+            out_descs=d_odescs.cpu().numpy().view(abi.DESC_DTYPE)[:n].copy(),
+            out_results=d_ores.cpu().numpy().view(abi.RESULT_DTYPE)[:n].copy(),
+            out_bytes=out_bytes)
+
     # -- multi-batch record sets (rpgpu_record_sets_plan_device / _run_device) ---------
     def record_sets(self, data: np.ndarray, sets: np.ndarray) -> dict:
         """kafka::batch_reader over many record sets on the GPU (device entry
