@@ -32,6 +32,8 @@
 //                        Kafka CRC of the decompressed body, then the header
 //                        CRC over the header carrying it; record walk; index
 //   decomp_patch_kernel  stores both CRCs into the rewritten headers
+#include <stdlib.h>
+
 #include "rpgpu_device.h"  // before rpgpu_codec.h: HIP attributes
 #include "rpgpu_codec.h"
 #include "rpgpu_zstd.h"
@@ -60,6 +62,13 @@ constexpr uint64_t kLitScratch = (128u << 10) + 256;  // ZSTD_BLOCKSIZE_MAX + sl
 #endif
 constexpr uint32_t kZstdLanes = RPZ_LANES;
 uint32_t zstd_lanes(uint32_t n) { return n < kZstdLanes ? n : kZstdLanes; }
+// lanes in flight for the lane decoders (tuning knobs for measurements:
+// RPGPU_LZ_LANES, RPGPU_ZSTD_LANES; the scratch is sized for zstd_lanes(n))
+uint32_t env_lanes(const char* name, uint32_t dflt) {
+    const char* e = getenv(name);
+    const long v = e ? atol(e) : 0;
+    return v > 0 && (uint64_t)v < dflt ? (uint32_t)v : dflt;
+}
 uint32_t decomp_waves(uint32_t n) { return n < kDecompWaves ? n : kDecompWaves; }
 // scratch: slot[n] u64 | local[n] u64 | block_sum[nb] u64 | validate scratch |
 //          counters (256 B) | wave literal scratch[waves] | lane Ws[lanes]
@@ -264,22 +273,23 @@ __global__ __launch_bounds__(256) void decomp_lane_kernel(
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
     rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
     rpgpu_batch_desc* __restrict__ out_descs) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const rpgpu_batch_desc d = descs[i];
-    const rpgpu_batch_result v = vres[i];
-    const bool want = decomp_wanted(d, v);
-    uint64_t sz = slot[i];
-    if (want && (v.codec == 4 || v.codec == 1 || wave_owned(d, v, sz))) return;  // ws_lane_kernel / decomp_wave_kernel
-    const uint64_t off = block_base[i / kScanBlock] + local[i];
-    int32_t verdict = RPGPU_V_SKIPPED;
-    uint64_t len = 0;
-    if (want && plan_slot(sz, off, out_cap, verdict)) {
-        rpcodec::DirectEmit em;
-        verdict = rpcodec::uncompress(em, v.codec, data + d.offset + kHeaderSize, body_len(v),
-                                      out + off + kHeaderSize, sz - kHeaderSize - rpcodec::kSlack, &len);
+    const uint32_t lanes = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += lanes) {
+        const rpgpu_batch_desc d = descs[i];
+        const rpgpu_batch_result v = vres[i];
+        const bool want = decomp_wanted(d, v);
+        uint64_t sz = slot[i];
+        if (want && (v.codec == 4 || v.codec == 1 || wave_owned(d, v, sz))) continue;  // ws_lane_kernel / decomp_wave_kernel
+        const uint64_t off = block_base[i / kScanBlock] + local[i];
+        int32_t verdict = RPGPU_V_SKIPPED;
+        uint64_t len = 0;
+        if (want && plan_slot(sz, off, out_cap, verdict)) {
+            rpcodec::DirectEmit em;
+            verdict = rpcodec::uncompress(em, v.codec, data + d.offset + kHeaderSize, body_len(v),
+                                          out + off + kHeaderSize, sz - kHeaderSize - rpcodec::kSlack, &len);
+        }
+        finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
     }
-    finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
 }
 
 // zstd batches up to kLaneMaxSlot (FAM 4) / all gzip batches (FAM 1): one lane
@@ -464,10 +474,13 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                                                               p.block_sum, d_dres, d_out, out_cap, d_out_descs,
                                                               p.counter, p.lits);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    decomp_lane_kernel<<<nblk, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
+    static const uint32_t lz_lanes = env_lanes("RPGPU_LZ_LANES", 1u << 30);
+    const uint32_t lzl = n < lz_lanes ? n : lz_lanes;
+    decomp_lane_kernel<<<(lzl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
                                             out_cap, d_out_descs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const uint32_t zl = zstd_lanes(n);
+    static const uint32_t zs_lanes = env_lanes("RPGPU_ZSTD_LANES", kZstdLanes);
+    const uint32_t zl = n < zs_lanes ? n : zs_lanes;
     ws_lane_kernel<4><<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
                                                          d_dres, d_out, out_cap, d_out_descs, p.zws);
     if ((e = hipGetLastError()) != hipSuccess) return e;

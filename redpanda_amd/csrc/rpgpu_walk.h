@@ -6,12 +6,11 @@
 // bytes/iobuf.cc:136-160 (short copies are silent, lengths truncate to int),
 // as restated by oracle/batch.c walk_records.
 //
-// The validate kernel checksums a group of up to 64 batches one after the
-// other (all 64 lanes on one batch), registering each batch that needs a
-// walk as a WalkJob in lane j of the group.  walk_lanes then walks all of
-// them at once, lane j over batch j.  The walk is a chain of dependent
-// reads (every field's position depends on the previous field's value), so
-// one batch per lane turns one wave's latency into 64 batches' progress.
+// walk_kernel (rpgpu_kernels.hip) runs after validate_kernel, one lane per
+// batch: walk_lanes walks the batch of every lane that validated OK and is
+// uncompressed.  The walk is a chain of dependent reads (every field's
+// position depends on the previous field's value), so one batch per lane
+// turns one wave's latency into 64 batches' progress.
 // Each lane reads its batch through a 32-byte register window reloaded at
 // the cursor when a field would run past it: for records with short keys,
 // one reload per record (at the header count, which the next record's
