@@ -120,12 +120,12 @@ __device__ __forceinline__ void coop_fill(uint8_t* dst, uint8_t b, uint64_t n, u
     }
 }
 
-// One group: lane k < cnt holds sequence k (literal run lsrc[0, ll), then a
-// match of ml bytes at distance off).  Out of line (called from every
+// One group: each lane with v holds one sequence (literal run lsrc[0, ll),
+// then a match of ml bytes at distance off), in lane order; lanes without v
+// hold none (and must carry ll = ml = 0).  Out of line (called from every
 // emission point of the decoders): the arguments travel in registers.
-__device__ __forceinline__ void exec_group(uint8_t* gbase, uint32_t cnt, const uint8_t* lsrc, uint64_t ll, uint64_t ml,
-                                        uint64_t off, uint32_t lid) {
-    const bool v = lid < cnt;
+__device__ __forceinline__ void exec_seqs(uint8_t* gbase, bool v, const uint8_t* lsrc, uint64_t ll, uint64_t ml,
+                                          uint64_t off, uint32_t lid) {
     const uint64_t tot = v ? ll + ml : 0;
     const uint64_t inc = wave_scan_incl(tot, lid);
     uint8_t* const o = gbase + (inc - tot);
@@ -157,6 +157,11 @@ __device__ __forceinline__ void exec_group(uint8_t* gbase, uint32_t cnt, const u
         }
         pend = pend && !ready;
     }
+}
+// lanes 0..cnt-1 hold the group's sequences
+__device__ __forceinline__ void exec_group(uint8_t* gbase, uint32_t cnt, const uint8_t* lsrc, uint64_t ll, uint64_t ml,
+                                           uint64_t off, uint32_t lid) {
+    exec_seqs(gbase, lid < cnt, lsrc, ll, ml, off, lid);
 }
 
 struct WaveEmit {
