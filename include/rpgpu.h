@@ -372,7 +372,11 @@ int32_t rpgpu_decomp_run_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_descs,
  * verdict OK / SKIPPED (not OK or already compressed) / DECOMP_OVERFLOW
  * (out_cap below the plan), out_offset, out_len (payload bytes), out_cap;
  * d_out_descs / d_out_results: the compressed batches and their validation
- * (crc, header_crc).  Other codecs: RPGPU_EINVAL. */
+ * (crc, header_crc).  Codec 1 (gzip, gzip_compressor.cc:106-172) and 4
+ * (zstd, stream_zstd.cc:89-151) produce valid streams that decode to the
+ * records bytes with zlib / libzstd and with this engine, but not the
+ * libraries' own bytes (fixed-Huffman deflate; raw literals with predefined
+ * FSE sequences).  Codec 0 or > 4: RPGPU_EINVAL. */
 size_t rpgpu_compress_scratch_bytes(uint32_t n);
 int32_t rpgpu_compress_plan_device(rpgpu_ctx* ctx, const rpgpu_batch_result* d_results, uint32_t n, int32_t codec,
                                    uint64_t* d_out_bytes, void* d_scratch, void* hip_stream);

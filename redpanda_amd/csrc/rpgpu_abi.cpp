@@ -432,7 +432,7 @@ size_t rpgpu_compress_scratch_bytes(uint32_t n) { return rpgpu::compress_scratch
 
 int32_t rpgpu_compress_plan_device(rpgpu_ctx* c, const rpgpu_batch_result* d_results, uint32_t n, int32_t codec,
                                    uint64_t* d_out_bytes, void* d_scratch, void* hip_stream) {
-    if (!c || (codec != 2 && codec != 3) || (n && (!d_results || !d_scratch))) return RPGPU_EINVAL;
+    if (!c || codec < 1 || codec > 4 || (n && (!d_results || !d_scratch))) return RPGPU_EINVAL;
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     hipError_t e = rpgpu::launch_compress_plan(d_results, n, (uint32_t)codec, d_out_bytes, d_scratch, s);
     if (e != hipSuccess) return fail(c, e, "compress plan launch");
@@ -444,7 +444,7 @@ int32_t rpgpu_compress_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs,
                                   rpgpu_decomp_result* d_cres, uint8_t* d_out, uint64_t out_cap,
                                   rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_out_results,
                                   void* d_scratch, void* hip_stream) {
-    if (!c || (codec != 2 && codec != 3) ||
+    if (!c || codec < 1 || codec > 4 ||
         (n && (!d_descs || !d_data || !d_results || !d_cres || !d_out || !d_out_descs || !d_out_results ||
                !d_scratch)))
         return RPGPU_EINVAL;

@@ -7,7 +7,9 @@
 // header gets attrs |= codec, size_bytes = 61 + payload, crc =
 // crc_record_batch and header_crc = internal_header_only_crc
 // (reset_size_checksum_metadata, :122-128).  LZ4 and snappy-java are
-// byte-identical to the reference's libraries (rpgpu_lz4c.h, rpgpu_snappyc.h).
+// byte-identical to the reference's libraries (rpgpu_lz4c.h, rpgpu_snappyc.h);
+// gzip and zstd are valid streams that round-trip (rpgpu_deflatec.h,
+// rpgpu_zstdc.h) but are not libzstd's / zlib's bytes.
 //
 //   compress_caps_kernel  one thread per batch: the output slot = 61-byte header
 //                         + the codec's bound + slack, and its exclusive scan
@@ -23,6 +25,8 @@
 #include "rpgpu_codec.h"
 #include "rpgpu_lz4c.h"
 #include "rpgpu_snappyc.h"
+#include "rpgpu_deflatec.h"
+#include "rpgpu_zstdc.h"
 
 namespace rpgpu {
 
@@ -36,10 +40,20 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
 size_t validate_scratch_bytes(uint32_t n);
 
 namespace {
-constexpr uint32_t kCompLanes = 131072;
+constexpr uint32_t kCompLanes = 131072, kEntropyLanes = 32768;
 constexpr uint64_t kTableBytes = rpsnapc::kMaxTable * 4;  // 64 KiB (LZ4 uses the first 32 KiB)
+constexpr uint64_t kZWsBytes = (sizeof(rpzstdc::Ws) + 255) & ~(uint64_t)255;
 constexpr uint64_t kCompSlack = 64;
-uint32_t comp_lanes(uint32_t n) { return n < kCompLanes ? n : kCompLanes; }
+// lanes in flight: gzip / zstd lanes (cold codecs) also carry a zstd work area
+uint32_t comp_lanes(uint32_t n, uint32_t codec) {
+    const uint32_t cap = (codec == 1 || codec == 4) ? kEntropyLanes : kCompLanes;
+    return n < cap ? n : cap;
+}
+__host__ __device__ constexpr uint64_t lane_stride(uint32_t codec) { return codec == 4 ? kTableBytes + kZWsBytes : kTableBytes; }
+uint64_t tables_bytes(uint32_t n) {
+    const uint64_t a = (uint64_t)comp_lanes(n, 3) * kTableBytes, b = (uint64_t)comp_lanes(n, 4) * lane_stride(4);
+    return a > b ? a : b;
+}
 struct CParts {
     uint64_t *slot, *local, *block_sum;
     void* vscratch;
@@ -62,13 +76,16 @@ CParts cparts(void* p, uint32_t n) {
 }
 }  // namespace
 
-size_t compress_scratch_bytes(uint32_t n) { return ctables_offset(n) + (size_t)comp_lanes(n) * kTableBytes; }
+size_t compress_scratch_bytes(uint32_t n) { return ctables_offset(n) + (size_t)tables_bytes(n); }
 
 __device__ __forceinline__ bool comp_wanted(const rpgpu_batch_result& v) {
     return v.verdict == RPGPU_V_OK && v.codec == 0;
 }
 __device__ __forceinline__ uint64_t comp_bound(uint32_t codec, uint64_t n) {
-    return codec == 3 ? rplz4c::frame_bound(n) : rpsnapc::stream_bound(n);
+    return codec == 3   ? rplz4c::frame_bound(n)
+           : codec == 2 ? rpsnapc::stream_bound(n)
+           : codec == 1 ? rpdefl::bound(n)
+                        : rpzstdc::bound(n);
 }
 
 __global__ __launch_bounds__(kScanBlock) void compress_caps_kernel(const rpgpu_batch_result* __restrict__ vres,
@@ -127,7 +144,10 @@ __global__ __launch_bounds__(256) void compress_lane_kernel(
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lanes = gridDim.x * blockDim.x;
     if (g >= n) return;
-    uint32_t* tab = tables + (uint64_t)g * (kTableBytes / 4);
+    uint8_t* lane = reinterpret_cast<uint8_t*>(tables) + (uint64_t)g * lane_stride(CODEC);
+    uint32_t* tab = reinterpret_cast<uint32_t*>(lane);
+    rpzstdc::Ws* zw = reinterpret_cast<rpzstdc::Ws*>(lane + kTableBytes);
+    if (CODEC == 4) rpzstdc::init_tables(*zw);
     uint32_t gen = 0;
     for (uint32_t i = g; i < n; i += lanes) {
         const rpgpu_batch_desc d = descs[i];
@@ -148,9 +168,17 @@ __global__ __launch_bounds__(256) void compress_lane_kernel(
                     rplz4c::Tab t{tab, gen};
                     len = rplz4c::compress_frame(p + kHeaderSize, body, o + kHeaderSize, t);
                     gen = t.gen;
-                } else {
+                } else if (CODEC == 2) {
                     rpsnapc::Tab t{tab, gen};
                     len = rpsnapc::compress_java(p + kHeaderSize, body, o + kHeaderSize, t);
+                    gen = t.gen;
+                } else if (CODEC == 1) {
+                    rpdefl::Tab t{tab, gen};
+                    len = rpdefl::compress(p + kHeaderSize, body, o + kHeaderSize, t);
+                    gen = t.gen;
+                } else {
+                    rpzstdc::Tab t{tab, gen};
+                    len = rpzstdc::compress(p + kHeaderSize, body, o + kHeaderSize, *zw, t);
                     gen = t.gen;
                 }
                 // the header of compress_batch (parser_utils.cc:107-113), on-disk
@@ -220,17 +248,19 @@ hipError_t launch_compress_run(const rpgpu_batch_desc* d_descs, uint32_t n, cons
                                hipStream_t s) {
     if (n == 0) return hipSuccess;
     const CParts p = cparts(d_scratch, n);
-    const uint32_t lanes = comp_lanes(n);
+    const uint32_t lanes = comp_lanes(n, codec);
     // tables from an earlier launch hold generations this one reuses: clear them
-    hipError_t e = hipMemsetAsync(p.tables, 0, (size_t)lanes * kTableBytes, s);
+    hipError_t e = hipMemsetAsync(p.tables, 0, (size_t)lanes * lane_stride(codec), s);
     if (e != hipSuccess) return e;
     const uint32_t blocks = (lanes + 255) / 256;
-    if (codec == 3)
-        compress_lane_kernel<3><<<blocks, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_cres,
-                                                       d_out, out_cap, d_out_descs, p.tables);
-    else
-        compress_lane_kernel<2><<<blocks, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_cres,
-                                                       d_out, out_cap, d_out_descs, p.tables);
+#define RPGPU_COMPRESS_LAUNCH(C)                                                                                  \
+    compress_lane_kernel<C><<<blocks, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_cres, \
+                                                   d_out, out_cap, d_out_descs, p.tables)
+    if (codec == 3) RPGPU_COMPRESS_LAUNCH(3);
+    else if (codec == 2) RPGPU_COMPRESS_LAUNCH(2);
+    else if (codec == 1) RPGPU_COMPRESS_LAUNCH(1);
+    else RPGPU_COMPRESS_LAUNCH(4);
+#undef RPGPU_COMPRESS_LAUNCH
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = launch_plan(d_out_descs, n, d_out, nullptr, p.vscratch, s)) != hipSuccess) return e;
     if ((e = launch_run(d_out_descs, n, d_out, d_vres2, nullptr, 0, p.vscratch, d_tables, grid, s, nullptr)) !=

@@ -13,6 +13,9 @@
 #include "rpgpu.h"
 #include "rpgpu_lz4c.h"
 #include "rpgpu_snappyc.h"
+#include "rpgpu_deflatec.h"
+#include "rpgpu_zstdc.h"
+#include "rpgpu_inflate.h"
 
 extern "C" {
 int32_t orc_compress(int codec, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
@@ -108,6 +111,77 @@ int main(int argc, char** argv) {
     // sizes around the boundaries: the 13-byte minimum, the 64 KB block, 1 MiB bodies
     static const size_t edge[] = {0, 1, 4, 11, 12, 13, 14, 17, 64, 255, 256, 4095, 4096, 65535, 65536, 65537, 65547,
                                   131072, 131073, 200000};
+    // gzip: round trip through zlib (the oracle's reference loop) and the engine's inflate
+    {
+        static rpinfl::Ws iws;
+        Bytes tab(rpdefl::kTable * 8);
+        rpdefl::Tab t{reinterpret_cast<uint32_t*>(tab.data()), 0};
+        for (long c = 0; c < cases + 40; c++) {
+            const size_t n = c < 40 ? edge[c % 20] : (below(3) == 0 ? below(1u << 20) : below(70000));
+            const Bytes in = payload(n);
+            Bytes z(rpdefl::bound(n) + 16);
+            const uint64_t zl = rpdefl::compress(in.data(), n, z.data(), t);
+            if (zl > rpdefl::bound(n)) {
+                fprintf(stderr, "gzip: %llu bytes over the bound %llu (n=%zu)\n", (unsigned long long)zl,
+                        (unsigned long long)rpdefl::bound(n), n);
+                return 1;
+            }
+            static Bytes back(2u << 20);
+            size_t bl = 0;
+            const int32_t v = orc_uncompress(1, z.data(), zl, back.data(), back.size(), &bl);
+            Bytes zp(z.begin(), z.begin() + zl);
+            zp.resize(zl + RPGPU_ARENA_TAIL_PAD);
+            Bytes back2(n + 64);
+            uint64_t bl2 = 0;
+            const int32_t v2 = rpinfl::uncompress(zp.data(), zl, back2.data(), n, &bl2, iws);
+            if (v != 0 || bl != n || (n && memcmp(back.data(), in.data(), n)) || v2 != 0 || bl2 != n ||
+                (n && memcmp(back2.data(), in.data(), n))) {
+                fprintf(stderr, "gzip round trip failed: n=%zu zlib v=%d len=%zu, engine v=%d len=%llu\n", n, v, bl, v2,
+                        (unsigned long long)bl2);
+                return 1;
+            }
+            n_cases++;
+        }
+    }
+    // zstd: round trip through libzstd (the oracle's reference loop) and the engine's decoder
+    {
+        static rpzstdc::Ws zw;
+        static rpzstd::Ws dw;
+        rpzstdc::init_tables(zw);
+        Bytes tab(rpzstdc::kTable * 8);
+        rpzstdc::Tab t{reinterpret_cast<uint32_t*>(tab.data()), 0};
+        for (long c = 0; c < cases + 40; c++) {
+            const size_t n = c < 40 ? edge[c % 20] : (below(3) == 0 ? below(1u << 20) : below(300000));
+            const Bytes in = payload(n);
+            Bytes z(rpzstdc::bound(n) + 16);
+            const uint64_t zl = rpzstdc::compress(in.data(), n, z.data(), zw, t);
+            if (zl > rpzstdc::bound(n)) {
+                fprintf(stderr, "zstd: %llu bytes over the bound (n=%zu)\n", (unsigned long long)zl, n);
+                return 1;
+            }
+            static Bytes back(2u << 20);
+            size_t bl = 0;
+            const int32_t v = orc_uncompress(4, z.data(), zl, back.data(), back.size(), &bl);
+            Bytes zp(z.begin(), z.begin() + zl);
+            zp.resize(zl + RPGPU_ARENA_TAIL_PAD);
+            Bytes back2(n + 64);
+            uint64_t bl2 = 0;
+            rpzstd::DirectEmit em;
+            const int32_t v2 = rpzstd::uncompress(em, zp.data(), zl, back2.data(), n, &bl2, dw);
+            if (v != 0 || bl != n || (n && memcmp(back.data(), in.data(), n)) || v2 != 0 || bl2 != n ||
+                (n && memcmp(back2.data(), in.data(), n))) {
+                fprintf(stderr, "zstd round trip failed: n=%zu libzstd v=%d len=%zu, engine v=%d len=%llu\n", n, v, bl,
+                        v2, (unsigned long long)bl2);
+                FILE* f = fopen("compress_fuzz_fail.bin", "wb");
+                if (f) {
+                    fwrite(in.data(), 1, n, f);
+                    fclose(f);
+                }
+                return 1;
+            }
+            n_cases++;
+        }
+    }
     for (int codec : {3, 2}) {
         for (size_t e : edge)
             for (int r = 0; r < 6; r++)

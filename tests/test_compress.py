@@ -3,7 +3,9 @@
 LZ4 frame and snappy-java are byte-identical to the reference's loops over
 liblz4 1.9.3 / snappy 1.1.8: the host build of the engine's restatements
 (rpgpu_lz4c.h, rpgpu_snappyc.h) is fuzzed against the oracle
-(tests/native/compress_fuzz.cpp), and the GPU path
+(tests/native/compress_fuzz.cpp; gzip and zstd, rpgpu_deflatec.h /
+rpgpu_zstdc.h, are round-tripped there through zlib / libzstd and the
+engine's decoders), and the GPU path
 (rpgpu_compress_plan_device / _run_device) is compared batch by batch with the
 oracle's compress_batch and round-tripped through the GPU decompressor."""
 import os
@@ -137,3 +139,47 @@ def test_gpu_compress_generated(eng, codec):
                                            int(cres["out_len"][i])].tobytes() != w]
     assert not bad, bad[:8]
     assert (cres["verdict"] == 0).sum() > 2900
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("codec", [1, 4])
+@pytest.mark.parametrize("fmt", [WIRE, DISK])
+def test_gpu_compress_round_trip_gzip_zstd(eng, codec, fmt):
+    """gzip / zstd: valid streams (not the libraries' bytes) -- the payload
+    decodes to the records bytes with zlib / libzstd through the reference's
+    loops and with the GPU decoder; the header fields are compress_batch's."""
+    import struct
+
+    data, descs = mixed_arena(20 + codec, 120, fmt)
+    got = eng.compress_arena(data, descs, codec)
+    res, cres = got["results"], got["cres"]
+    want = orc.compress_batches(data, descs, res, 3)  # only for which batches are compressed
+    for i, w in enumerate(want):
+        if w is None:
+            assert cres["verdict"][i] == abi.V_SKIPPED, i
+            continue
+        assert cres["verdict"][i] == 0, (i, cres["verdict"][i])
+        o, m = int(cres["out_offset"][i]), int(cres["out_len"][i])
+        b = got["out"][o:o + 61 + m].tobytes()
+        s = int(descs["offset"][i])
+        body = data[s + 61:s + int(res["size_bytes"][i])].tobytes()
+        v, dec = orc.uncompress(codec, b[61:], cap=len(body) + 1024)
+        assert v == 0 and dec == body, i
+        # every header field but crc / header_crc / size / attrs equals the oracle's (LZ4) rewrite
+        hw = np.frombuffer(w[:61], dtype=abi.RP_HEADER_DTYPE)[0]
+        hg = np.frombuffer(b[:61], dtype=abi.RP_HEADER_DTYPE)[0]
+        assert int(hg["size_bytes"]) == 61 + m and int(hg["attrs"]) == (int(hw["attrs"]) & ~7) | codec
+        for f in ("base_offset", "type", "last_offset_delta", "first_timestamp", "max_timestamp", "producer_id",
+                  "producer_epoch", "base_sequence", "record_count"):
+            assert hg[f] == hw[f], f
+        assert int(hg["crc"]) == orc.crc_record_batch(hg, b[61:])
+        assert int(hg["header_crc"]) == orc.internal_header_only_crc(hg)
+    ok = np.nonzero(cres["verdict"] == 0)[0]
+    od = got["out_descs"][ok].copy()
+    od["ops"] = abi.OPS_PRODUCE | abi.OP_DECOMP
+    back = eng.decompress_arena(got["out"], od)
+    assert (back["dres"]["verdict"] == 0).all()
+    for k, i in enumerate(ok):
+        a, m = int(back["dres"]["out_offset"][k]), int(back["dres"]["out_len"][k])
+        s = int(descs["offset"][i])
+        assert back["out"][a + 61:a + 61 + m].tobytes() == data[s + 61:s + int(res["size_bytes"][i])].tobytes()
