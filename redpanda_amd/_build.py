@@ -43,10 +43,19 @@ def _run(cmd: list[str]) -> None:
 def build_rpgpu(force: bool = False) -> Path:
     srcs = [CSRC / s for s in RPGPU_SRCS + RPGPU_HDRS] + [INCLUDE / "rpgpu.h"]
     if force or _stale(LIBRPGPU, srcs):
+        # one hipcc per translation unit, in parallel, then one link
+        from concurrent.futures import ThreadPoolExecutor
+
+        obj = ROOT / "build" / "obj"
+        obj.mkdir(parents=True, exist_ok=True)
+        flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", f"-I{INCLUDE}", f"-I{CSRC}"]
+        objs = [obj / (s + ".o") for s in RPGPU_SRCS]
+        jobs = max(1, min(len(objs), os.cpu_count() or 1, 8))
+        with ThreadPoolExecutor(jobs) as ex:
+            list(ex.map(lambda so: _run(["hipcc", *flags, "-c", str(CSRC / so[0]), "-o", str(so[1])]),
+                        zip(RPGPU_SRCS, objs)))
         tmp = LIBRPGPU.with_suffix(".so.tmp")
-        _run(["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              f"-I{INCLUDE}", f"-I{CSRC}", *[str(CSRC / s) for s in RPGPU_SRCS],
-              "-o", str(tmp)])
+        _run(["hipcc", f"--offload-arch={ARCH}", "-shared", *[str(o) for o in objs], "-o", str(tmp)])
         os.replace(tmp, LIBRPGPU)
     return LIBRPGPU
 

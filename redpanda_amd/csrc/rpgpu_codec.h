@@ -151,10 +151,43 @@ RPC_HD void copy_match(uint8_t* dst, uint64_t off, uint64_t n) {
 // within kSlack); the device's wave-cooperative emitter (rpgpu_wave.h)
 // collects 64 sequences and executes them with the whole wavefront.
 struct DirectEmit {
+#if defined(RPGPU_DIAG_NOCOPY)  // diagnostics builds only: the parse without its copies
+    RPC_HD void lits(uint8_t*, const uint8_t*, uint64_t) {}
+    RPC_HD void match(uint8_t*, uint64_t, uint64_t) {}
+#elif defined(RPGPU_DIAG_STOREONLY)  // ... with the stores and no loads
+    RPC_HD void put(uint8_t* dst, uint64_t n) {
+        B16 v = {0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u};
+        for (uint64_t i = 0; i < n; i += 16) st16(dst + i, v);
+    }
+    RPC_HD void lits(uint8_t* dst, const uint8_t*, uint64_t n) { put(dst, n); }
+    RPC_HD void match(uint8_t* dst, uint64_t, uint64_t n) { put(dst, n); }
+#elif defined(RPGPU_DIAG_LOADONLY)  // ... with the loads, whose values are waited for, and no stores
+    RPC_HD void get(uint8_t* dst, const uint8_t* src, uint64_t n) {
+        for (uint64_t i = 0; i < n; i += 16) {
+            B16 v;
+            ld16(v, src + i);
+            if (v[0] == 0x9E3779B9u && v[1] == 0x7F4A7C15u) st16(dst, v);
+        }
+    }
+    RPC_HD void lits(uint8_t* dst, const uint8_t* src, uint64_t n) { get(dst, src, n); }
+    RPC_HD void match(uint8_t* dst, uint64_t off, uint64_t n) { get(dst, dst - off, n); }
+#else
     RPC_HD void lits(uint8_t* dst, const uint8_t* src, uint64_t n) { copy_fwd(dst, src, n); }
     RPC_HD void match(uint8_t* dst, uint64_t off, uint64_t n) { copy_match(dst, off, n); }
+#endif
     RPC_HD void sync() {}
 };
+// DirectEmit whose LZ4 blocks take lz4_block_lane (the lane kernels' form)
+struct LaneEmit : DirectEmit {};
+template <class E>
+struct IsLane {
+    static constexpr bool value = false;
+};
+template <>
+struct IsLane<LaneEmit> {
+    static constexpr bool value = true;
+};
+constexpr int64_t kInPad = 64;  // readable bytes past an input's end (RPGPU_ARENA_TAIL_PAD)
 
 // ---------------------------------------------------------------- input window
 // The decoders read tokens, lengths and offsets through 32 bytes of input
@@ -337,6 +370,280 @@ RPC_HD int64_t lz4_block(E& em, const uint8_t* in, int64_t isz, uint8_t* out, in
     }
 }
 
+// ------------------------------------------------------ LZ4 block, lane form
+// The same decoder (liblz4's acceptance, check for check, as lz4_block above)
+// shaped for a GPU lane that decodes one block while 63 other lanes of its
+// wavefront decode theirs in lockstep.  There, time is set by the dependent
+// memory round trips per sequence -- every lane of the wave waits for the
+// slowest -- not by instructions.  lz4_block spends several per sequence (a
+// window reload, the literal load, the match load, each behind the previous
+// store); this form spends one:
+//   - tokens, lengths and offsets are read from a 64-byte register window
+//     whose next 32 bytes are prefetched a step ahead;
+//   - a sequence with <= 32 literal bytes and a match of <= 48 bytes whose
+//     source lies before it (offset >= 16 per 16-byte chunk), or any match
+//     with offset < 16 (a period rebuilt in registers), issues all its loads
+//     at once -- literal bytes, the match source's chunks -- and composes the
+//     match bytes that come from this sequence's own literal run from
+//     registers (those bytes are not stored yet when the loads issue);
+//   - the stores follow (16-byte wild stores as liblz4's, each sequence's
+//     overwriting the previous one's overshoot).
+// Longer runs take lz4_block's copies.  Host-compiled by the differential
+// fuzz test (tests/native/codec_fuzz.cpp) against the oracle.
+struct V16 {
+    uint64_t lo, hi;
+};
+RPC_HD V16 v16_ld(const uint8_t* p) {
+    B16 v;
+    ld16(v, p);
+    return V16{((uint64_t)v[1] << 32) | v[0], ((uint64_t)v[3] << 32) | v[2]};
+}
+RPC_HD void v16_st(uint8_t* p, const V16& x) {
+    B16 v;
+    v[0] = (uint32_t)x.lo, v[1] = (uint32_t)(x.lo >> 32), v[2] = (uint32_t)x.hi, v[3] = (uint32_t)(x.hi >> 32);
+    st16(p, v);
+}
+RPC_HD uint64_t funnel(uint64_t a, uint64_t b, uint32_t s) {  // bytes [s, s + 8) of a|b, s < 8
+    return s ? (a >> (8 * s)) | (b << (64 - 8 * s)) : a;
+}
+// bytes [r, r + 16) of the 32 bytes x|y (bytes past 32 read as zero), r < 32
+RPC_HD V16 v16_ext(const V16& x, const V16& y, uint32_t r) {
+    const uint32_t k = r >> 3, s = r & 7;
+    const uint64_t a = k == 0 ? x.lo : k == 1 ? x.hi : k == 2 ? y.lo : y.hi;
+    const uint64_t b = k == 0 ? x.hi : k == 1 ? y.lo : k == 2 ? y.hi : 0;
+    const uint64_t c = k == 0 ? y.lo : k == 1 ? y.hi : 0;
+    return V16{funnel(a, b, s), funnel(b, c, s)};
+}
+// x moved up by t bytes (t <= 16), zeros shifted in
+RPC_HD V16 v16_shl(const V16& x, uint32_t t) { return v16_ext(V16{0, 0}, x, 16 - t); }
+// bytes [0, k) of a, [k, 16) of b (k <= 16)
+RPC_HD V16 v16_merge(const V16& a, const V16& b, uint32_t k) {
+    const uint64_t ml = k >= 8 ? ~0ull : (1ull << (8 * k)) - 1;
+    const uint64_t mh = k >= 16 ? ~0ull : k > 8 ? (1ull << (8 * (k - 8))) - 1 : 0ull;
+    return V16{(a.lo & ml) | (b.lo & ~ml), (a.hi & mh) | (b.hi & ~mh)};
+}
+
+// 64 input bytes [pos, pos + 64) in registers plus the next 32 in flight
+struct Win64 {
+    uint32_t w0, w1, w2, w3, w4, w5, w6, w7, w8, w9, w10, w11, w12, w13, w14, w15;
+    uint32_t n0, n1, n2, n3, n4, n5, n6, n7;  // [npos, npos + 32)
+    int32_t pos, npos;  // block offsets (a block is < 2^31 bytes)
+};
+RPC_HD void w64_prefetch(Win64& W, const uint8_t* in, int32_t lim) {
+    // [pos + 64, +32), clamped so no read passes lim (the input's readable end)
+    const int32_t p = W.pos + 64 + 32 <= lim ? W.pos + 64 : -1;
+    W.npos = p;
+    if (p >= 0) {
+        B16 a, b;
+        ld16(a, in + p);
+        ld16(b, in + p + 16);
+        W.n0 = a[0], W.n1 = a[1], W.n2 = a[2], W.n3 = a[3], W.n4 = b[0], W.n5 = b[1], W.n6 = b[2], W.n7 = b[3];
+    }
+}
+RPC_HD void w64_load(Win64& W, const uint8_t* in, int32_t p, int32_t lim) {
+    if (p > lim - 64) p = lim - 64;  // lim >= 64: the block is followed by the arena's tail padding
+    B16 a, b, c, d;
+    ld16(a, in + p);
+    ld16(b, in + p + 16);
+    ld16(c, in + p + 32);
+    ld16(d, in + p + 48);
+    W.w0 = a[0], W.w1 = a[1], W.w2 = a[2], W.w3 = a[3], W.w4 = b[0], W.w5 = b[1], W.w6 = b[2], W.w7 = b[3];
+    W.w8 = c[0], W.w9 = c[1], W.w10 = c[2], W.w11 = c[3], W.w12 = d[0], W.w13 = d[1], W.w14 = d[2], W.w15 = d[3];
+    W.pos = p;
+    w64_prefetch(W, in, lim);
+}
+// the window advances by 32 bytes onto the prefetched ones
+RPC_HD void w64_shift(Win64& W, const uint8_t* in, int32_t lim) {
+    W.w0 = W.w8, W.w1 = W.w9, W.w2 = W.w10, W.w3 = W.w11, W.w4 = W.w12, W.w5 = W.w13, W.w6 = W.w14, W.w7 = W.w15;
+    W.w8 = W.n0, W.w9 = W.n1, W.w10 = W.n2, W.w11 = W.n3, W.w12 = W.n4, W.w13 = W.n5, W.w14 = W.n6, W.w15 = W.n7;
+    W.pos += 32;
+    w64_prefetch(W, in, lim);
+}
+// dword q (0..16; 16 reads as 0) of the window: a select tree
+RPC_HD uint32_t w64_dword(const Win64 W, uint32_t q) {  // by value: keeps W out of scratch memory
+    const bool o = q & 1;
+    const uint32_t a0 = o ? W.w1 : W.w0, a1 = o ? W.w3 : W.w2, a2 = o ? W.w5 : W.w4, a3 = o ? W.w7 : W.w6;
+    const uint32_t a4 = o ? W.w9 : W.w8, a5 = o ? W.w11 : W.w10, a6 = o ? W.w13 : W.w12, a7 = o ? W.w15 : W.w14;
+    const bool t = q & 2;
+    const uint32_t b0 = t ? a1 : a0, b1 = t ? a3 : a2, b2 = t ? a5 : a4, b3 = t ? a7 : a6;
+    const uint32_t c0 = (q & 4) ? b1 : b0, c1 = (q & 4) ? b3 : b2;
+    return q >= 16 ? 0u : ((q & 8) ? c1 : c0);
+}
+// 4 input bytes from p (little-endian), [p, p + need) inside the window
+// (reloaded there if not: a dependent load, off the common path)
+RPC_HD uint32_t w64_at(Win64& W, const uint8_t* in, int32_t p, int32_t need, int32_t lim) {
+    if (p < W.pos || p + need > W.pos + 64) w64_load(W, in, p, lim);
+    const uint32_t o = (uint32_t)(p - W.pos), q = o >> 2, sh = 8 * (o & 3);
+    const uint32_t lo = w64_dword(W, q);
+    return sh ? (lo >> sh) | (w64_dword(W, q + 1) << (32 - sh)) : lo;
+}
+RPC_HD uint32_t lz4_varlen64(Win64& W, const uint8_t* in, int32_t& ip, int32_t lencheck, bool initial_check,
+                             int& err, int32_t lim) {
+    uint32_t len = 0;
+    err = 0;
+    if (initial_check && ip >= lencheck) {
+        err = 1;
+        return 0;
+    }
+    uint32_t s;
+    do {
+        s = w64_at(W, in, ip, 1, lim) & 255u;
+        ip++;
+        len += s;
+        if (ip >= lencheck) {
+            err = 2;
+            return len;
+        }
+    } while (s == 255);
+    return len;
+}
+
+// Returns the decoded size, or -1 (lz4_block's contract).  `lim` = bytes of
+// `in` that may be read (the block plus the arena's tail padding).
+RPC_HD int32_t lz4_block_lane(const uint8_t* in, int32_t isz, uint8_t* out, int32_t ocap, int32_t hist,
+                              int32_t lim) {
+    if (isz == 0) return -1;
+    const int32_t iend = isz, oend = ocap;
+    const bool check_off = hist < 65536;
+    int32_t ip = 0, op = 0;
+    bool safe = oend < 64;
+    int err;
+    Win64 W;
+    w64_load(W, in, 0, lim);
+    for (;;) {
+        // keep the token and the fields after it inside the window
+        if (ip >= W.pos + 32) {
+            if (ip < W.pos + 64 && W.npos == W.pos + 64) w64_shift(W, in, lim);
+            else w64_load(W, in, ip, lim);
+        }
+        // ---- parse one sequence (lz4_block's decisions): literal run
+        // in[ip_lit, +ll) at out[op], then unless `last` a match of ml
+        // bytes at distance off
+        const uint32_t token = w64_at(W, in, ip, 1, lim) & 255u;
+        ip++;
+        int32_t ll = token >> 4, ml = token & 15, off = 0, ip_lit = ip;
+        bool lit_checks = false, last = false, shortcut = false, lits_taken = false;
+        if (!safe) {
+            if (ll == 15) {
+                ll += lz4_varlen64(W, in, ip, iend - 15, true, err, lim);
+                if (err == 1) return -1;
+                lit_checks = op + ll > oend - 32 || ip + ll > iend - 32;
+            } else {
+                lit_checks = ip > iend - 17;
+            }
+            if (lit_checks) safe = true;
+        } else if (ll != 15 && ip < iend - 16 && op <= oend - 32) {
+            // two-stage shortcut: literals, then either a short match at once
+            // or the general match path
+            lits_taken = true;
+            ip_lit = ip;
+            ip += ll;
+            off = w64_at(W, in, ip, 2, lim) & 0xFFFFu;
+            ip += 2;
+            shortcut = ml != 15 && off >= 8 && off <= op + ll + hist;
+        } else {
+            if (ll == 15) {
+                ll += lz4_varlen64(W, in, ip, iend - 15, true, err, lim);
+                if (err == 1) return -1;
+            }
+            lit_checks = true;
+        }
+        if (!lits_taken) {
+            ip_lit = ip;
+            if (lit_checks && (op + ll > oend - 12 || ip + ll > iend - 8)) {
+                // MFLIMIT / input parsing restriction: must be the last literals
+                if (ip + ll != iend || op + ll > oend) return -1;
+                last = true;
+            } else {
+                ip += ll;
+                off = w64_at(W, in, ip, 2, lim) & 0xFFFFu;
+                ip += 2;
+            }
+        }
+        const int32_t op_m = op + ll;
+        if (!last) {
+            if (shortcut) {
+                ml += 4;
+            } else {
+                if (ml == 15) {
+                    ml += lz4_varlen64(W, in, ip, iend - 4, false, err, lim);  // iend - LASTLITERALS + 1
+                    if (err) return -1;
+                }
+                ml += 4;  // MINMATCH
+                if (!safe && op_m + ml >= oend - 64) safe = true;  // goto safe_match_copy
+                if (check_off && off > op_m + hist) return -1;     // offset outside buffers
+                if (safe && op_m + ml > oend - 5) return -1;       // last LASTLITERALS bytes are literals
+            }
+        }
+        // ---- copies
+        const bool pat = off < 16;
+        const int32_t nch = pat ? 1 : (ml + 15) >> 4;
+        if (last || ll > 32 || (!pat && (ml > 48 || off < 16 * nch))) {
+            if (ll) copy_fwd(out + op, in + ip_lit, (uint64_t)ll);
+            if (last) return op + ll;
+            copy_match(out + op_m, (uint64_t)off, (uint64_t)ml);
+            op = op_m + ml;
+            continue;
+        }
+        // one round trip: every load of the sequence, then its stores
+        const int32_t rel = ll - off;  // match source start - literal start
+        const uint8_t* src = out + op_m - off;
+        V16 L0{0, 0}, L1{0, 0}, A0{0, 0}, A1{0, 0}, A2{0, 0};
+        if (ll > 0) L0 = v16_ld(in + ip_lit);
+        if (ll > 16) L1 = v16_ld(in + ip_lit + 16);
+        if (off != 0 && rel < 0) A0 = v16_ld(src);
+        if (!pat && nch > 1 && rel + 16 < 0) A1 = v16_ld(src + 16);
+        if (!pat && nch > 2 && rel + 32 < 0) A2 = v16_ld(src + 32);
+        if (ll > 0) v16_st(out + op, L0);
+        if (ll > 16) v16_st(out + op + 16, L1);
+        // 16 source bytes at literal-relative r: stored bytes (A) below the
+        // literal run, the run's own bytes (registers) from it on
+        const int32_t r0 = rel, r1 = rel + 16, r2 = rel + 32;
+        const V16 c0 = r0 >= 0 ? v16_ext(L0, L1, (uint32_t)r0)
+                       : r0 <= -16 ? A0 : v16_merge(A0, v16_shl(L0, (uint32_t)-r0), (uint32_t)-r0);
+        if (pat) {
+            // period-off pattern (off 0: liblz4's zeros), stored a whole
+            // number of periods apart
+            uint64_t lo = 0, hi = 0, step = 16;
+            if (off != 0) {
+                lo = c0.lo;
+                hi = c0.hi;
+                if (off <= 8) {
+                    if (off < 8) lo &= (1ull << (8 * off)) - 1;
+                    hi = 0;
+                } else {
+                    hi &= (1ull << (8 * (off - 8))) - 1;
+                }
+                for (uint64_t w = (uint64_t)off; w < 16; w *= 2) {
+                    const uint64_t sh = 8 * w;
+                    if (sh < 64) {
+                        hi |= (hi << sh) | (lo >> (64 - sh));
+                        lo |= lo << sh;
+                    } else {
+                        hi |= lo << (sh - 64);
+                    }
+                }
+                step = (uint64_t)off * (16 / (uint64_t)off);
+            }
+            const V16 pv{lo, hi};
+            for (uint64_t i = 0; i < (uint64_t)ml; i += step) v16_st(out + op_m + i, pv);
+        } else {
+            v16_st(out + op_m, c0);
+            if (nch > 1) {
+                const V16 c1 = r1 >= 0 ? v16_ext(L0, L1, (uint32_t)r1)
+                               : r1 <= -16 ? A1 : v16_merge(A1, v16_shl(L0, (uint32_t)-r1), (uint32_t)-r1);
+                v16_st(out + op_m + 16, c1);
+            }
+            if (nch > 2) {
+                const V16 c2 = r2 >= 0 ? v16_ext(L0, L1, (uint32_t)r2)
+                               : r2 <= -16 ? A2 : v16_merge(A2, v16_shl(L0, (uint32_t)-r2), (uint32_t)-r2);
+                v16_st(out + op_m + 32, c2);
+            }
+        }
+        op = op_m + ml;
+    }
+}
+
 // ---------------------------------------------------------------- LZ4 frame
 enum { kLz4Error = 0, kLz4Partial = 1, kLz4Skip = 2, kLz4Frame = 3 };
 constexpr uint32_t kLz4Magic = 0x184D2204u, kLz4SkipMagic = 0x184D2A50u;
@@ -475,7 +782,13 @@ RPC_HD int32_t lz4f_uncompress(E& em, const uint8_t* in, uint64_t n, uint8_t* ou
             *out_len = o;
             return V_OVERFLOW;
         }
-        const int64_t d = lz4_block(em, in + pos, (int64_t)size, out + o, f.max_block, f.linked ? (int64_t)o : 0);
+        int64_t d;
+        if constexpr (IsLane<E>::value)
+            d = lz4_block_lane(in + pos, (int32_t)size, out + o, (int32_t)f.max_block,
+                               f.linked ? (int32_t)(o < 65536 ? o : 65536) : 0,
+                               (int32_t)((n - pos < size + kInPad ? n - pos : size + kInPad) + kInPad));
+        else
+            d = lz4_block(em, in + pos, (int64_t)size, out + o, f.max_block, f.linked ? (int64_t)o : 0);
         if (d < 0) return V_ERROR;  // decompressionFailed
         const uint64_t s = o;
         o += (uint64_t)d;

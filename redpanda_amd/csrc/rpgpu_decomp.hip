@@ -64,13 +64,6 @@ constexpr uint32_t kZstdLanes = RPZ_LANES;
 uint32_t zstd_lanes(uint32_t n) { return n < kZstdLanes ? n : kZstdLanes; }
 // lanes in flight for the lane decoders (tuning knobs for measurements:
 // RPGPU_LZ_LANES, RPGPU_ZSTD_LANES; the scratch is sized for zstd_lanes(n))
-bool two_phase_on() {
-    static const bool on = [] {
-        const char* e = getenv("RPGPU_TWO_PHASE");
-        return e && atoi(e) != 0;
-    }();
-    return on;
-}
 uint32_t env_lanes(const char* name, uint32_t dflt) {
     const char* e = getenv(name);
     const long v = e ? atol(e) : 0;
@@ -85,7 +78,6 @@ union LaneWs {
 };
 struct Parts {
     uint64_t *slot, *local, *block_sum;
-    uint32_t* nrec;  // sequence records per two-phase batch (kNoRecords: none)
     uint32_t* wlist; // wave-owned batches: zstd [0, n), LZ [n, 2n)
     void* vscratch;
     uint32_t* counter;
@@ -94,7 +86,7 @@ struct Parts {
 };
 size_t parts_head(uint32_t n) {
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
-    return ((size_t)n * 28 + nb * 8 + 255) & ~(size_t)255;
+    return ((size_t)n * 24 + nb * 8 + 255) & ~(size_t)255;  // slot, local: 8 B; wlist: 2 x 4 B
 }
 size_t counter_offset(uint32_t n) { return (parts_head(n) + validate_scratch_bytes(n) + 255) & ~(size_t)255; }
 size_t zws_offset(uint32_t n) { return counter_offset(n) + 256 + (size_t)decomp_waves(n) * kLitScratch; }
@@ -104,8 +96,7 @@ Parts parts(void* p, uint32_t n) {
     s.slot = reinterpret_cast<uint64_t*>(b);
     s.local = s.slot + n;
     s.block_sum = s.local + n;
-    s.nrec = reinterpret_cast<uint32_t*>(s.block_sum + (n + kScanBlock - 1) / kScanBlock);
-    s.wlist = s.nrec + n;
+    s.wlist = reinterpret_cast<uint32_t*>(s.block_sum + (n + kScanBlock - 1) / kScanBlock);
     s.vscratch = b + parts_head(n);
     s.counter = reinterpret_cast<uint32_t*>(b + counter_offset(n));
     s.lits = b + counter_offset(n) + 256;
@@ -127,83 +118,6 @@ constexpr uint64_t kOverCeiling = 1ull << 63;
 __device__ __forceinline__ bool decomp_wanted(const rpgpu_batch_desc& d, const rpgpu_batch_result& v) {
     return (d.ops & RPGPU_OP_DECOMP) && v.verdict == RPGPU_V_OK && v.codec != 0;
 }
-
-// Two-phase LZ4 / snappy decode (lane-sized batches): decomp_lane_kernel runs
-// the restatement with RecEmit, which stores each sequence as a 16-byte
-// record (literal source, literal length, match length, offset) behind the
-// batch's output slot; lz_exec_kernel then executes the records with the
-// whole wave, 64 at a time (rpwave::exec_group): literal and match bytes move
-// in coalesced runs instead of one lane's 16-byte accesses.  The record area
-// holds one record per 8 slot bytes; a batch that needs more (or whose
-// decoder reads its own output: an LZ4 content checksum) is decoded directly
-// by its lane instead.
-constexpr uint32_t kNoRecords = 0xFFFFFFFFu;
-constexpr uint32_t kJump = 0xFFFFFFFFu;  // record.y of a "next sequence at x" record
-__device__ __forceinline__ bool two_phase(uint32_t codec, uint64_t sz) {
-    return (codec == 2 || codec == 3) && sz <= kLaneMaxSlot;
-}
-__device__ __forceinline__ uint64_t rec_cap(uint64_t sz) { return sz / 8 + 16; }
-__device__ __forceinline__ uint64_t rec_bytes(uint64_t sz) { return rec_cap(sz) * 16; }
-
-struct RecEmit {
-    uint8_t* obase;        // decoded body: dst pointers are taken relative to it
-    const uint8_t* ibase;  // the batch body (literal sources)
-    uint4* rec;
-    uint32_t cap, n;
-    uint64_t expect;       // dst offset of the next sequence
-    uint32_t plo, pll;     // literal run waiting for its match
-    bool has_lit, bad;
-    __device__ __forceinline__ void init(uint8_t* o, const uint8_t* i, uint4* r, uint32_t c) {
-        obase = o;
-        ibase = i;
-        rec = r;
-        cap = c;
-        n = 0;
-        expect = 0;
-        plo = pll = 0;
-        has_lit = bad = false;
-    }
-    __device__ __forceinline__ void put(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-        if (n < cap) rec[n] = make_uint4(a, b, c, d);
-        else bad = true;
-        n++;
-    }
-    __device__ __forceinline__ void flush_lit() {
-        if (has_lit) {
-            put(plo, pll, 0, 0);
-            has_lit = false;
-        }
-    }
-    __device__ __forceinline__ void place(uint64_t o) {
-        if (o != expect) {
-            flush_lit();
-            put((uint32_t)o, kJump, 0, 0);
-            expect = o;
-        }
-    }
-    __device__ __forceinline__ void lits(uint8_t* dst, const uint8_t* src, uint64_t len) {
-        flush_lit();
-        const uint64_t o = (uint64_t)(dst - obase);
-        place(o);
-        plo = (uint32_t)(src - ibase);
-        pll = (uint32_t)len;
-        has_lit = true;
-        expect = o + len;
-    }
-    __device__ __forceinline__ void match(uint8_t* dst, uint64_t off, uint64_t len) {
-        const uint64_t o = (uint64_t)(dst - obase);
-        if (!has_lit || o != expect) {
-            flush_lit();
-            place(o);
-            plo = pll = 0;
-        }
-        put(plo, pll, (uint32_t)len, (uint32_t)off);
-        has_lit = false;
-        expect = o + len;
-    }
-    __device__ __forceinline__ void sync() { bad = true; }  // the decoder reads its output
-    __device__ __forceinline__ void finish() { flush_lit(); }
-};
 
 __device__ __forceinline__ uint64_t body_len(const rpgpu_batch_result& v) {
     return (uint64_t)(uint32_t)v.size_bytes - kHeaderSize;  // verdict OK: 61 <= size_bytes <= length
@@ -231,7 +145,7 @@ __global__ __launch_bounds__(256) void gzip_bound_kernel(const rpgpu_batch_desc*
 __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
     const rpgpu_batch_result* __restrict__ vres, uint64_t* __restrict__ slot, uint64_t* __restrict__ local,
-    uint64_t* __restrict__ block_sum, uint64_t max_decoded, bool tp, uint32_t* __restrict__ wcount,
+    uint64_t* __restrict__ block_sum, uint64_t max_decoded, uint32_t* __restrict__ wcount,
     uint32_t* __restrict__ wlist) {
     __shared__ uint64_t wsum[kScanBlock / 64];
     const uint32_t i = blockIdx.x * kScanBlock + threadIdx.x;
@@ -253,8 +167,7 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
             }
         }
     }
-    // the two-phase decode's record area follows the slot
-    const uint64_t span = sz + (tp && sz && i < n && two_phase(vres[i].codec, sz) ? rec_bytes(sz) : 0);
+    const uint64_t span = sz;
     const uint32_t l = lane_id();
     uint64_t x = span;
 #pragma unroll
@@ -364,287 +277,50 @@ __device__ __forceinline__ bool wave_owned(const rpgpu_batch_desc& d, const rpgp
 
 // LZ4 (CODEC 3, which also writes the verdict of every batch nobody decodes)
 // or snappy (CODEC 2) batches up to kLaneMaxSlot, one lane each; one instance
-// per codec keeps each at its own register count (lanes in flight are what
-// bounds these latency-bound decodes).  TP: the two-phase variant (records
-// for lz_exec_kernel, RPGPU_TWO_PHASE=1).
+// per codec keeps each at its own register count.  Lanes in flight bound these
+// latency-bound decodes: at <= 128 VGPRs (4 waves per SIMD) a C3-sized arena's
+// lanes are all resident at once.  LZ4 blocks take rpcodec::lz4_block_lane
+// (one memory round trip per sequence).  The descriptor and validation result
+// are read again after the decode (reread()) instead of being held in
+// registers across it.
 #ifndef RPGPU_LANE_WAVES
-#define RPGPU_LANE_WAVES 1
+#define RPGPU_LANE_WAVES 4
 #endif
-template <uint32_t CODEC, bool TP>
+template <class T>
+__device__ __forceinline__ const T* reread(const T* p) {  // the compiler may not reuse loads through p
+    uint64_t x = (uint64_t)p;
+    asm volatile("" : "+s"(x));
+    return reinterpret_cast<const T*>(x);
+}
+template <uint32_t CODEC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_WAVES))) void decomp_lane_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
     const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
     rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
-    rpgpu_batch_desc* __restrict__ out_descs, uint32_t* __restrict__ nrec) {
+    rpgpu_batch_desc* __restrict__ out_descs) {
     const uint32_t lanes = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += lanes) {
-        const rpgpu_batch_desc d = descs[i];
-        const rpgpu_batch_result v = vres[i];
-        const bool want = decomp_wanted(d, v);
-        uint64_t sz = slot[i];
-        uint32_t nr = kNoRecords;
-        // this instance's batches: its codec's lane-sized ones (+ for LZ4, the undecoded)
-        const bool mine = want ? (v.codec == CODEC && !wave_owned(d, v, sz)) : CODEC == 3;
-        if (mine) {
-            const uint64_t off = block_base[i / kScanBlock] + local[i];
-            int32_t verdict = RPGPU_V_SKIPPED;
-            uint64_t len = 0;
+        uint64_t sz = slot[i], off = 0;
+        int32_t verdict = RPGPU_V_SKIPPED;
+        uint64_t len = 0;
+        {
+            const rpgpu_batch_desc d = descs[i];
+            const rpgpu_batch_result v = vres[i];
+            const bool want = decomp_wanted(d, v);
+            // this instance's batches: its codec's lane-sized ones (+ for LZ4, the undecoded)
+            const bool mine = want ? (v.codec == CODEC && !wave_owned(d, v, sz)) : CODEC == 3;
+            if (!mine) continue;
+            off = block_base[i / kScanBlock] + local[i];
             if (want && plan_slot(sz, off, out_cap, verdict)) {
                 const uint8_t* in = data + d.offset + kHeaderSize;
                 uint8_t* o = out + off + kHeaderSize;
                 const uint64_t cap = sz - kHeaderSize - rpcodec::kSlack;
-                bool direct = true;
-                if (TP && two_phase(v.codec, sz) && off + sz + rec_bytes(sz) <= out_cap) {
-                    RecEmit em;
-                    em.init(o, in, reinterpret_cast<uint4*>(out + off + sz), (uint32_t)rec_cap(sz));
-                    verdict = rpcodec::uncompress(em, CODEC, in, body_len(v), o, cap, &len);
-                    em.finish();
-                    if (!em.bad) {
-                        nr = em.n;
-                        direct = false;
-                    }
-                }
-                if (direct) {
-                    rpcodec::DirectEmit em;
-                    verdict = rpcodec::uncompress(em, CODEC, in, body_len(v), o, cap, &len);
-                }
-            }
-            finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
-        }
-        if (TP && mine) nrec[i] = nr;
-    }
-}
-
-// Phase 2 of the two-phase decode: one wavefront per batch (grid-stride), the
-// records 64 at a time.  A group whose output fits kLdsGroup bytes runs in an
-// LDS ring that also holds the last kLdsHist bytes before it: literals are
-// loaded from the input into the ring, matches are resolved in rounds
-// (rpwave's rule: a match may copy once no pending match of the group writes
-// bytes its source reads) by byte copies inside the ring -- or from the output
-// in HBM when the source is older than the ring -- and the group's bytes go to
-// HBM in aligned 16-byte chunks.  Dependent back-references then wait on LDS,
-// not on L2.  Larger groups (long runs) take rpwave::exec_seqs in HBM.
-using rpcodec::B16;
-constexpr uint32_t kRing = 4096, kRingMask = kRing - 1;
-constexpr uint64_t kLdsGroup = 2048, kLdsHist = kRing - kLdsGroup;
-
-__device__ __forceinline__ void b16_split(const B16& v, uint64_t& lo, uint64_t& hi) {
-    lo = ((uint64_t)v[1] << 32) | v[0];
-    hi = ((uint64_t)v[3] << 32) | v[2];
-}
-// bytes [h, 16) of lo|hi moved down to byte 0
-__device__ __forceinline__ void shr_bytes(uint64_t& lo, uint64_t& hi, uint32_t h) {
-    if (h >= 8) {
-        lo = hi >> (8 * (h - 8));
-        hi = 0;
-    } else if (h) {
-        lo = (lo >> (8 * h)) | (hi << (64 - 8 * h));
-        hi >>= 8 * h;
-    }
-}
-
-// LDS accesses of 8 / 16 bytes off their natural alignment are correct on
-// gfx950 (replayed at ~64 cycles per wave-instruction, cdna_hip_programming.md
-// Guideline 17), far cheaper than a dependent byte per LDS round trip.
-__device__ __forceinline__ void lds_put(uint8_t* ring, uint64_t idx, uint64_t lo, uint64_t hi, uint32_t n) {
-    // exactly n (<= 16) bytes of lo|hi at ring[idx...] (mod kRing)
-    idx &= kRingMask;
-    if (idx + 16 <= kRing) {
-        uint8_t* p = ring + idx;
-        if (n == 16) {
-            B16 v;
-            v[0] = (uint32_t)lo, v[1] = (uint32_t)(lo >> 32), v[2] = (uint32_t)hi, v[3] = (uint32_t)(hi >> 32);
-            *reinterpret_cast<B16*>(p) = v;
-            return;
-        }
-        if (n & 8) {
-            *reinterpret_cast<uint64_t*>(p) = lo;
-            p += 8;
-            lo = hi;
-        }
-        if (n & 4) {
-            *reinterpret_cast<uint32_t*>(p) = (uint32_t)lo;
-            p += 4;
-            lo >>= 32;
-        }
-        if (n & 2) {
-            *reinterpret_cast<uint16_t*>(p) = (uint16_t)lo;
-            p += 2;
-            lo >>= 16;
-        }
-        if (n & 1) *p = (uint8_t)lo;
-        return;
-    }
-    for (uint32_t j = 0; j < n; j++) ring[(idx + j) & kRingMask] = (uint8_t)(j < 8 ? lo >> (8 * j) : hi >> (8 * (j - 8)));
-}
-__device__ __forceinline__ void lds_get(const uint8_t* ring, uint64_t idx, uint64_t& lo, uint64_t& hi) {
-    idx &= kRingMask;
-    if (idx + 16 <= kRing) {
-        const B16 v = *reinterpret_cast<const B16*>(ring + idx);
-        b16_split(v, lo, hi);
-        return;
-    }
-    lo = hi = 0;
-    for (uint32_t j = 0; j < 16; j++) {
-        const uint64_t c = ring[(idx + j) & kRingMask];
-        if (j < 8) lo |= c << (8 * j);
-        else hi |= c << (8 * (j - 8));
-    }
-}
-
-__device__ __forceinline__ void ring_group(uint8_t* __restrict__ ring, uint32_t* pmap, uint8_t* obase, uint32_t afix, uint64_t P,
-                                           uint64_t hist, uint64_t T, bool v, const uint8_t* lsrc, uint64_t ll,
-                                           uint64_t ml, uint64_t off, uint64_t o, uint32_t lid) {
-    const uint64_t old = P - hist;  // positions below: HBM only
-    // 1. literals into the ring
-    if (v && ll) {
-        for (uint64_t k = 0; k < ll; k += 16) {
-            B16 x;
-            rpcodec::ld16(x, lsrc + k);
-            uint64_t lo, hi;
-            b16_split(x, lo, hi);
-            lds_put(ring, o + k + afix, lo, hi, (uint32_t)(ll - k < 16 ? ll - k : 16));
-        }
-    }
-    wave_lds_sync();
-    // 2. matches, in rounds of true dependencies: a byte bitmap over the
-    // group's output marks the bytes pending matches still owe; a match copies
-    // once no byte of its source is pending (the first pending match always
-    // qualifies), then clears its own bytes
-    const uint64_t mo = o + ll;
-    bool pend = v && ml > 0;
-    pmap[lid] = 0;
-    wave_lds_sync();
-    if (pend) {
-        const uint64_t a = mo - P, e = a + ml;  // group-relative, e <= T <= kLdsGroup
-        for (uint64_t w = a >> 5; w <= (e - 1) >> 5; w++) {
-            const uint64_t lo = w * 32 > a ? w * 32 : a, hi = w * 32 + 32 < e ? w * 32 + 32 : e;
-            const uint32_t m = (uint32_t)(((hi - lo) >= 32 ? ~0ull : ((1ull << (hi - lo)) - 1)) << (lo - w * 32));
-            atomicOr(pmap + w, m);
-        }
-    }
-    wave_lds_sync();
-    const uint64_t slo = mo - off, shi0 = slo + ml;
-    const uint64_t shi = shi0 < mo ? shi0 : mo;
-    while (rpwave::ballot(pend)) {
-        bool ready = false;
-        if (pend) {
-            ready = true;
-            if (off != 0 && shi > P) {
-                const uint64_t a = slo > P ? slo - P : 0, e = shi - P;
-                for (uint64_t w = a >> 5; ready && w <= (e - 1) >> 5; w++) {
-                    const uint64_t lo = w * 32 > a ? w * 32 : a, hi = w * 32 + 32 < e ? w * 32 + 32 : e;
-                    const uint32_t m =
-                        (uint32_t)(((hi - lo) >= 32 ? ~0ull : ((1ull << (hi - lo)) - 1)) << (lo - w * 32));
-                    ready = (pmap[w] & m) == 0;
-                }
+                rpcodec::LaneEmit em;  // LZ4 blocks: lz4_block_lane
+                verdict = rpcodec::uncompress(em, CODEC, in, body_len(v), o, cap, &len);
             }
         }
-        if (ready) {
-            if (off == 0) {  // liblz4's offset 0: zeros
-                for (uint64_t k = 0; k < ml; k += 16) lds_put(ring, mo + k + afix, 0, 0, (uint32_t)(ml - k < 16 ? ml - k : 16));
-            } else if (shi0 <= old) {  // the whole source is older than the ring: HBM
-                for (uint64_t k = 0; k < ml; k += 16) {
-                    B16 x;
-                    rpcodec::ld16(x, obase + slo + k);
-                    uint64_t lo, hi;
-                    b16_split(x, lo, hi);
-                    lds_put(ring, mo + k + afix, lo, hi, (uint32_t)(ml - k < 16 ? ml - k : 16));
-                }
-            } else if (off >= 16 && slo >= old) {  // in the ring, 16 bytes at a time
-                for (uint64_t k = 0; k < ml; k += 16) {
-                    uint64_t lo, hi;
-                    lds_get(ring, slo + k + afix, lo, hi);
-                    lds_put(ring, mo + k + afix, lo, hi, (uint32_t)(ml - k < 16 ? ml - k : 16));
-                }
-            } else {  // short period or straddling the ring's start: bytes
-                for (uint64_t j = 0; j < ml; j++) {
-                    const uint64_t sp = slo + j;
-                    const uint8_t c = sp < old ? obase[sp] : ring[(sp + afix) & kRingMask];
-                    ring[(mo + j + afix) & kRingMask] = c;
-                }
-            }
-        }
-        wave_lds_sync();
-        if (ready) {  // the bytes are there: clear them from the bitmap
-            const uint64_t a = mo - P, e = a + ml;
-            for (uint64_t w = a >> 5; w <= (e - 1) >> 5; w++) {
-                const uint64_t lo = w * 32 > a ? w * 32 : a, hi = w * 32 + 32 < e ? w * 32 + 32 : e;
-                const uint32_t m = (uint32_t)(((hi - lo) >= 32 ? ~0ull : ((1ull << (hi - lo)) - 1)) << (lo - w * 32));
-                atomicAnd(pmap + w, ~m);
-            }
-        }
-        pend = pend && !ready;
-        wave_lds_sync();
-    }
-    // 3. [P, P + T) to HBM, aligned 16-byte chunks (ring index = address mod 16)
-    const uint64_t a0 = ((uint64_t)(obase + P)) & ~(uint64_t)15, a1 = (uint64_t)(obase + P + T);
-    for (uint64_t c = a0 + 16 * (uint64_t)lid; c < a1; c += 1024) {
-        const uint64_t q = c - (uint64_t)obase;  // may be "negative" for the head chunk: modular ring index
-        const B16 x = *reinterpret_cast<const B16*>(ring + ((q + afix) & kRingMask));
-        const uint64_t lo_b = c < (uint64_t)(obase + P) ? (uint64_t)(obase + P) - c : 0;  // skip bytes before P
-        const uint64_t hi_b = a1 - c < 16 ? a1 - c : 16;
-        if (lo_b == 0 && hi_b == 16) {
-            rpcodec::st16(reinterpret_cast<uint8_t*>(c), x);
-        } else {
-            uint64_t lo, hi;
-            b16_split(x, lo, hi);
-            shr_bytes(lo, hi, (uint32_t)lo_b);
-            rpzstd::st_part(reinterpret_cast<uint8_t*>(c + lo_b), lo, hi, hi_b - lo_b);
-        }
-    }
-}
-
-__global__ __launch_bounds__(64) void lz_exec_kernel(const rpgpu_batch_desc* __restrict__ descs, uint32_t n,
-                                                     const uint8_t* __restrict__ data,
-                                                     const uint64_t* __restrict__ slot,
-                                                     const uint64_t* __restrict__ local,
-                                                     const uint64_t* __restrict__ block_base,
-                                                     const uint32_t* __restrict__ nrec, uint8_t* out) {
-    __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
-    __shared__ uint32_t pmap[kLdsGroup / 32];  // pending-byte bitmap of the group
-    const uint32_t lid = lane_id();
-    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const uint32_t nr = nrec[i];
-        if (nr == kNoRecords || nr == 0) continue;
-        const uint64_t sz = slot[i];
-        const uint64_t off = block_base[i / kScanBlock] + local[i];
-        uint8_t* const obase = out + off + kHeaderSize;
-        const uint32_t afix = (uint32_t)((uint64_t)obase & 15);
-        const uint4* rec = reinterpret_cast<const uint4*>(out + off + sz);
-        const uint8_t* in = data + descs[i].offset + kHeaderSize;
-        uint64_t P = 0, hist = 0;
-        for (uint32_t b = 0; b < nr; b += 64) {
-            const uint32_t cnt = nr - b < 64 ? nr - b : 64;
-            uint4 r = make_uint4(0, 0, 0, 0);
-            if (lid < cnt) r = rec[b + lid];
-            uint64_t jumps = rpwave::ballot(lid < cnt && r.y == kJump);
-            uint32_t start = 0;
-            for (;;) {
-                const uint32_t stop = jumps ? (uint32_t)__builtin_ctzll(jumps) : cnt;
-                const bool v = lid >= start && lid < stop;
-                const uint64_t ll = v ? r.y : 0, ml = v ? r.z : 0;
-                const uint64_t tot = ll + ml;
-                const uint64_t inc = rpwave::wave_scan_incl(tot, lid);
-                const uint64_t T = rpwave::readlane64(inc, 63);
-                const bool small = T <= kLdsGroup && !rpwave::ballot(ll > 256);
-                if (small) {
-                    ring_group(ring, pmap, obase, afix, P, hist, T, v, in + r.x, ll, ml, r.w, P + inc - tot, lid);
-                    hist = hist + T < kLdsHist ? hist + T : kLdsHist;
-                } else {
-                    rpwave::exec_seqs(obase + P, v, in + r.x, ll, ml, r.w, lid);
-                    hist = 0;
-                }
-                P += T;
-                if (stop == cnt) break;
-                P = (uint32_t)__builtin_amdgcn_readlane((int)r.x, (int)stop);
-                hist = 0;
-                start = stop + 1;
-                jumps &= jumps - 1;
-            }
-        }
-        wave_lds_sync();  // the next batch reuses the ring
+        finish_batch(i, reread(descs)[i], reread(vres)[i], off, sz, verdict, len, data, out, dres, out_descs);
     }
 }
 
@@ -653,8 +329,11 @@ __global__ __launch_bounds__(64) void lz_exec_kernel(const rpgpu_batch_desc* __r
 // (Huffman / FSE tables) in HBM.  gzip is decoded bit-serially as zlib does;
 // no benchmark configuration carries it, so it has no wave
 // decoder.  One instance per codec keeps each at its own register count.
+#ifndef RPGPU_WS_WAVES
+#define RPGPU_WS_WAVES 1
+#endif
 template <uint32_t FAM>
-__global__ __launch_bounds__(256) void ws_lane_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_WS_WAVES))) void ws_lane_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
     const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
@@ -804,7 +483,7 @@ hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const
     // wave-owned batch lists (filled by decomp_caps_kernel): counters 2 and 3
     if ((e = hipMemsetAsync(p.counter + 2, 0, 2 * sizeof(uint32_t), s)) != hipSuccess) return e;
     decomp_caps_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
-                                                 max_decoded, two_phase_on(), p.counter + 2, p.wlist);
+                                                 max_decoded, p.counter + 2, p.wlist);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_block_scan(p.block_sum, nb, d_out_bytes, s);
@@ -839,20 +518,10 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     static const uint32_t lz_lanes = env_lanes("RPGPU_LZ_LANES", 1u << 30);
     const uint32_t lzl = n < lz_lanes ? n : lz_lanes;
     const uint32_t lzb = (lzl + 255) / 256;
-    if (two_phase_on()) {
-        if ((e = hipMemsetAsync(p.nrec, 0xFF, (size_t)n * sizeof(uint32_t), s)) != hipSuccess) return e;
-        decomp_lane_kernel<3, true><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
-                                                        d_dres, d_out, out_cap, d_out_descs, p.nrec);
-        decomp_lane_kernel<2, true><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
-                                                        d_dres, d_out, out_cap, d_out_descs, p.nrec);
-        const uint32_t xw = n < 32768 ? n : 32768;
-        lz_exec_kernel<<<xw, 64, 0, s>>>(d_descs, n, d_data, p.slot, p.local, p.block_sum, p.nrec, d_out);
-    } else {
-        decomp_lane_kernel<3, false><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
-                                                         d_dres, d_out, out_cap, d_out_descs, p.nrec);
-        decomp_lane_kernel<2, false><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
-                                                         d_dres, d_out, out_cap, d_out_descs, p.nrec);
-    }
+    decomp_lane_kernel<3><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
+                                              out_cap, d_out_descs);
+    decomp_lane_kernel<2><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
+                                              out_cap, d_out_descs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     static const uint32_t zs_lanes = env_lanes("RPGPU_ZSTD_LANES", kZstdLanes);
     const uint32_t zl = n < zs_lanes ? n : zs_lanes;

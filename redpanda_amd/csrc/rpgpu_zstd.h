@@ -702,8 +702,13 @@ struct Huf4 {
 // scratch buffer and executes sequences 64 at a time with the whole wave.
 struct DirectEmit {
     static constexpr bool kInlineBlocks = false;
+#ifdef RPGPU_DIAG_NOCOPY  // diagnostics build only: the decode without its sequence copies
+    RPC_HD void lits(uint8_t*, const uint8_t*, uint64_t) {}
+    RPC_HD void match(uint8_t*, uint64_t, uint64_t) {}
+#else
     RPC_HD void lits(uint8_t* dst, const uint8_t* src, uint64_t n) { copy_lits(dst, src, n); }
     RPC_HD void match(uint8_t* dst, uint64_t off, uint64_t n) { copy_seq_match(dst, off, n); }
+#endif
     RPC_HD void fill(uint8_t* dst, uint8_t v, uint64_t n) { fill_bytes(dst, v, n); }
     RPC_HD void sync() {}
     // where a block's Huffman / RLE literals are decoded

@@ -1,5 +1,5 @@
 # C3 step time per library variant (build/var/*.so via RPGPU_DIAG_LIB) and the
-# two-phase switch; first the parity tests on the default build
+# first the parity tests on the default build
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -13,7 +13,6 @@ run() {  # label, env...
   python -c "import json; d=json.load(open('gpurun_out/var_$label.json')); print('$CFG $label', d['ms_per_step'], d['value'], d['roofline']['frac'])"
 }
 run base
-run tp RPGPU_TWO_PHASE=1
 for f in build/var/*.so; do
   run $(basename $f .so) RPGPU_DIAG_LIB=$PWD/$f
 done

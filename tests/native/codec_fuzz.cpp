@@ -339,6 +339,21 @@ void check(int codec, const Bytes& in, const char* what, long id) {
     uint64_t glen = 0;
     rpcodec::DirectEmit em;
     const int32_t gv = rpcodec::uncompress(em, (uint32_t)codec, ib.data(), n, ob.data(), bound, &glen);
+    // the lane kernels' LZ4 block form (lz4_block_lane): same verdict, length and bytes
+    {
+        Bytes lb(bound + rpcodec::kSlack + (g_exact ? 0 : 64), 0x5A);
+        uint64_t llen = 0;
+        rpcodec::LaneEmit le;
+        const int32_t lv = rpcodec::uncompress(le, (uint32_t)codec, ib.data(), n, lb.data(), bound, &llen);
+        if (lv != gv || (gv == 0 && (llen != glen || (glen && memcmp(lb.data(), ob.data(), glen))))) {
+            size_t fd = 0;
+            while (fd < glen && lb[fd] == ob[fd]) fd++;
+            fprintf(stderr, "LANE DIVERGENCE case %ld (%s) codec %d: direct %d len %llu, lane %d len %llu, first diff %zu\n", id, what,
+                    codec, gv, (unsigned long long)glen, lv, (unsigned long long)llen, fd);
+            if (getenv("DUMP")) { FILE* f = fopen("/tmp/case.bin", "wb"); fwrite(in.data(), 1, n, f); fclose(f); }
+            exit(1);
+        }
+    }
     const size_t ocap = bound + (1u << 20);
     Bytes rb(ocap);
     size_t rlen = 0;
