@@ -144,6 +144,78 @@ RPC_HD void copy_match(uint8_t* dst, uint64_t off, uint64_t n) {
     for (uint64_t i = 0; i < n; i += step) st16(dst + i, p);
 }
 
+// n < 16 bytes of lo|hi, exactly
+RPC_HD void st_part(uint8_t* p, uint64_t lo, uint64_t hi, uint64_t n) {
+    if (n & 8) {
+        __builtin_memcpy(p, &lo, 8);
+        p += 8;
+        lo = hi;
+    }
+    if (n & 4) {
+        const uint32_t v = (uint32_t)lo;
+        __builtin_memcpy(p, &v, 4);
+        p += 4;
+        lo >>= 32;
+    }
+    if (n & 2) {
+        const uint16_t v = (uint16_t)lo;
+        __builtin_memcpy(p, &v, 2);
+        p += 2;
+        lo >>= 16;
+    }
+    if (n & 1) *p = (uint8_t)lo;
+}
+// Exact copies (nothing written past dst + n), for outputs whose next bytes
+// another lane may already have written (split blocks and chunks).
+RPC_HD void copy_exact(uint8_t* dst, const uint8_t* src, uint64_t n) {  // disjoint ranges
+    uint64_t i = 0;
+    for (; i + 16 <= n; i += 16) {
+        B16 v;
+        ld16(v, src + i);
+        st16(dst + i, v);
+    }
+    if (i < n) st_part(dst + i, le64(src + i), le64(src + i + 8), n - i);
+}
+RPC_HD void match_exact(uint8_t* dst, uint64_t off, uint64_t n) {  // dst[i] = dst[i - off]; off 0: zeros
+    if (off >= 16) {
+        uint64_t i = 0;
+        for (; i + 16 <= n; i += 16) {
+            B16 v;
+            ld16(v, dst - off + i);
+            st16(dst + i, v);
+        }
+        if (i < n) st_part(dst + i, le64(dst - off + i), le64(dst - off + i + 8), n - i);
+        return;
+    }
+    uint64_t lo = 0, hi = 0, step = 16;
+    if (off != 0) {
+        const uint8_t* s = dst - off;
+        lo = le64(s);
+        hi = le64(s + 8);
+        if (off <= 8) {
+            if (off < 8) lo &= (1ull << (8 * off)) - 1;
+            hi = 0;
+        } else {
+            hi &= (1ull << (8 * (off - 8))) - 1;
+        }
+        for (uint64_t w = off; w < 16; w *= 2) {
+            const uint64_t sh = 8 * w;
+            if (sh < 64) {
+                hi |= (hi << sh) | (lo >> (64 - sh));
+                lo |= lo << sh;
+            } else {
+                hi |= lo << (sh - 64);
+            }
+        }
+        step = off * (16 / off);
+    }
+    B16 p;
+    p[0] = (uint32_t)lo, p[1] = (uint32_t)(lo >> 32), p[2] = (uint32_t)hi, p[3] = (uint32_t)(hi >> 32);
+    uint64_t i = 0;
+    for (; i + 16 <= n; i += step) st16(dst + i, p);
+    if (i < n) st_part(dst + i, lo, hi, n - i);
+}
+
 // ---------------------------------------------------------------- emitters
 // The decoders below decide everything -- acceptance, lengths, offsets --
 // from the input alone and hand every literal run and back-reference to an
@@ -188,6 +260,20 @@ struct IsLane<LaneEmit> {
     static constexpr bool value = true;
 };
 constexpr int64_t kInPad = 64;  // readable bytes past an input's end (RPGPU_ARENA_TAIL_PAD)
+// DirectEmit that writes nothing at or past `end` (a split chunk's output
+// bound): copies within 64 bytes of it are exact
+struct BoundEmit {
+    uint8_t* end;
+    RPC_MF void lits(uint8_t* dst, const uint8_t* src, uint64_t n) {
+        if (dst + n + 64 <= end) copy_fwd(dst, src, n);
+        else copy_exact(dst, src, n);
+    }
+    RPC_MF void match(uint8_t* dst, uint64_t off, uint64_t n) {
+        if (dst + n + 64 <= end) copy_match(dst, off, n);  // copy_fwd for off >= 64: 64-byte steps
+        else match_exact(dst, off, n);
+    }
+    RPC_MF void sync() {}
+};
 
 // ---------------------------------------------------------------- input window
 // The decoders read tokens, lengths and offsets through 32 bytes of input
@@ -578,10 +664,12 @@ RPC_HD int32_t lz4_block_lane(const uint8_t* in, int32_t isz, uint8_t* out, int3
         // ---- copies
         const bool pat = off < 16;
         const int32_t nch = pat ? 1 : (ml + 15) >> 4;
-        if (last || ll > 32 || (!pat && (ml > 48 || off < 16 * nch))) {
-            if (ll) copy_fwd(out + op, in + ip_lit, (uint64_t)ll);
+        if (last || ll > 32 || (!pat && (ml > 48 || off < 16 * nch)) || op_m + ml + 15 > oend) {
+            // exact copies: nothing is written past the block's capacity
+            // (a split frame's next block may already be there)
+            if (ll) copy_exact(out + op, in + ip_lit, (uint64_t)ll);
             if (last) return op + ll;
-            copy_match(out + op_m, (uint64_t)off, (uint64_t)ml);
+            match_exact(out + op_m, (uint64_t)off, (uint64_t)ml);
             op = op_m + ml;
             continue;
         }
@@ -980,6 +1068,97 @@ RPC_HD uint64_t snappy_java_bound(const uint8_t* x, uint64_t n) {
         pos += take;
     }
     return b;
+}
+
+// ---------------------------------------------------------------- split plans
+// A large body whose parts decode independently -- the blocks of an LZ4
+// frame with independent blocks (the reference's own compressor writes
+// them, lz4_frame_compressor.cc:74-76, as Kafka's Java client does), the
+// chunks of a snappy-java body (one per iobuf fragment,
+// snappy_java_compressor.cc:58-75) -- is decoded one part per lane instead
+// of serially.  A plan is made only for bodies whose whole structure is
+// regular: every part present in full, no checksums to verify, nothing after
+// the end mark; each part's output goes where the serial decode would put it
+// if every LZ4 block but the last decodes to maxBlockSize (snappy chunks
+// carry their exact length).  Anything else -- and any plan whose parts do
+// not come back as assumed -- is decoded serially, so verdicts and bytes are
+// the serial restatement's.  emit(k, kind, in_off, in_len, out_off, out_cap,
+// hdr) is called once per part; returns the number of parts (0: no plan).
+enum { kPartLz4Block = 0, kPartLz4Stored = 1, kPartSnappy = 2 };
+template <class F>
+RPC_HD uint32_t lz4f_split(const uint8_t* in, uint64_t n, uint32_t max_parts, F&& emit) {
+    const Lz4Frame f = lz4f_header(in, n);
+    if (f.kind != kLz4Frame || f.linked || f.block_sum || f.content_sum) return 0;
+    uint64_t pos = f.hlen, o = 0;
+    uint32_t k = 0;
+    for (;;) {
+        if (n - pos < 4) return 0;
+        const uint32_t bh = le32(in + pos);
+        pos += 4;
+        if (bh == 0) return pos == n ? k : 0;
+        const uint64_t size = bh & 0x7FFFFFFFu;
+        if (size > f.max_block || n - pos < size || k >= max_parts) return 0;
+        const bool stored = (bh & 0x80000000u) != 0;
+        emit(k, stored ? kPartLz4Stored : kPartLz4Block, pos, size, o, stored ? size : (uint64_t)f.max_block, 0u);
+        o += stored ? size : f.max_block;
+        pos += size;
+        k++;
+    }
+}
+template <class F>
+RPC_HD uint32_t snappy_java_split(const uint8_t* x, uint64_t n, uint32_t max_parts, F&& emit) {
+    if (n < 16 || !snappy_java_magic(x) || (int32_t)le32(x + 12) < 1) return 0;
+    uint64_t pos = 16, o = 0;
+    uint32_t k = 0;
+    while (pos != n) {
+        if (n - pos < 4 || k >= max_parts) return 0;
+        const int32_t clen = (int32_t)be32(x + pos);
+        pos += 4;
+        if (clen < 0 || (uint64_t)clen > n - pos || (uint32_t)clen > (64u << 20)) return 0;
+        uint32_t u, used;
+        if (!snappy_varint(x + pos, (uint64_t)clen, u, used)) return 0;
+        emit(k, kPartSnappy, pos, (uint64_t)clen, o, (uint64_t)u, used);
+        o += u;
+        pos += (uint64_t)clen;
+        k++;
+    }
+    return k;
+}
+// One part: its decoded size, or -1.  `in` = the part's bytes (readable
+// kInPad bytes past in_len), `out` = its output (nothing is written at or
+// past out + out_cap).
+RPC_HD int64_t decode_part(uint32_t kind, const uint8_t* in, uint64_t in_len, uint8_t* out, uint64_t out_cap,
+                           uint32_t hdr) {
+    if (kind == kPartLz4Block)
+        return lz4_block_lane(in, (int32_t)in_len, out, (int32_t)out_cap, 0, (int32_t)(in_len + kInPad));
+    if (kind == kPartLz4Stored) {
+        copy_exact(out, in, in_len);
+        return (int64_t)in_len;
+    }
+    BoundEmit em{out + out_cap};
+    return snappy_raw(em, in, in_len, out, (uint32_t)out_cap, hdr) ? (int64_t)out_cap : -1;
+}
+// The serial verdict of a planned body whose parts all decoded: OK and the
+// total length, or false (the body goes to the serial decoder).  r(k) = part
+// k's decoded size.
+template <class R>
+RPC_HD bool split_result(uint32_t codec, const uint8_t* in, uint64_t n, uint32_t parts, R&& r, uint64_t* len) {
+    uint64_t o = 0;
+    bool ok = true;
+    auto check = [&](uint32_t k, uint32_t kind, uint64_t, uint64_t, uint64_t out_off, uint64_t out_cap, uint32_t) {
+        const int64_t d = r(k);
+        if (d < 0 || (kind == kPartLz4Block && k + 1 < parts && (uint64_t)d != out_cap)) ok = false;
+        o = out_off + (d < 0 ? 0 : (uint64_t)d);
+    };
+    if (codec == 3) {
+        if (lz4f_split(in, n, parts, check) != parts) return false;
+        const Lz4Frame f = lz4f_header(in, n);
+        if (f.content != 0 && o != f.content) ok = false;  // frameSize_wrong: the serial decoder's verdict
+    } else {
+        if (snappy_java_split(in, n, parts, check) != parts) return false;
+    }
+    *len = o;
+    return ok;
 }
 
 // ---------------------------------------------------------------- dispatch

@@ -76,9 +76,20 @@ union LaneWs {
     rpzstd::Ws z;
     rpinfl::Ws g;
 };
+// one part of a split body (rpcodec::lz4f_split / snappy_java_split)
+struct SplitPart {
+    uint32_t batch, kind, in_off, in_len;  // offsets within the batch body
+    uint64_t out_off;                      // within the decoded body
+    uint32_t out_cap, hdr;
+};
+// parts in flight: LZ4 parts in [0, cap / 2), snappy's in [cap / 2, cap)
+uint32_t part_cap(uint32_t n) { return 2 * ((n + 4096u) / 2); }
 struct Parts {
     uint64_t *slot, *local, *block_sum;
-    uint32_t* wlist; // wave-owned batches: zstd [0, n), LZ [n, 2n)
+    uint32_t* wlist;   // wave-owned batches: zstd [0, n), LZ [n, 2n)
+    uint32_t *sfirst, *scount;  // a split batch's parts (scount 0: not split)
+    SplitPart* parts;
+    int32_t* pres;     // decoded size per part (-1 error, -2 no slot)
     void* vscratch;
     uint32_t* counter;
     uint8_t* lits;
@@ -86,10 +97,13 @@ struct Parts {
 };
 size_t parts_head(uint32_t n) {
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
-    return ((size_t)n * 24 + nb * 8 + 255) & ~(size_t)255;  // slot, local: 8 B; wlist: 2 x 4 B
+    return ((size_t)n * 32 + nb * 8 + 255) & ~(size_t)255;  // slot, local: 8 B; wlist: 2 x 4 B; sfirst, scount
 }
 size_t counter_offset(uint32_t n) { return (parts_head(n) + validate_scratch_bytes(n) + 255) & ~(size_t)255; }
 size_t zws_offset(uint32_t n) { return counter_offset(n) + 256 + (size_t)decomp_waves(n) * kLitScratch; }
+size_t parts_offset(uint32_t n) {
+    return (zws_offset(n) + (size_t)zstd_lanes(n) * sizeof(LaneWs) + 255) & ~(size_t)255;
+}
 Parts parts(void* p, uint32_t n) {
     uint8_t* b = static_cast<uint8_t*>(p);
     Parts s;
@@ -97,15 +111,21 @@ Parts parts(void* p, uint32_t n) {
     s.local = s.slot + n;
     s.block_sum = s.local + n;
     s.wlist = reinterpret_cast<uint32_t*>(s.block_sum + (n + kScanBlock - 1) / kScanBlock);
+    s.sfirst = s.wlist + 2 * (size_t)n;
+    s.scount = s.sfirst + n;
     s.vscratch = b + parts_head(n);
     s.counter = reinterpret_cast<uint32_t*>(b + counter_offset(n));
     s.lits = b + counter_offset(n) + 256;
     s.zws = reinterpret_cast<LaneWs*>(b + zws_offset(n));
+    s.parts = reinterpret_cast<SplitPart*>(b + parts_offset(n));
+    s.pres = reinterpret_cast<int32_t*>(s.parts + part_cap(n));
     return s;
 }
 }  // namespace
 
-size_t decomp_scratch_bytes(uint32_t n) { return zws_offset(n) + (size_t)zstd_lanes(n) * sizeof(LaneWs); }
+size_t decomp_scratch_bytes(uint32_t n) {
+    return parts_offset(n) + (size_t)part_cap(n) * (sizeof(SplitPart) + sizeof(int32_t));
+}
 
 // slots above this go to the wave decoders (a lane's serial decode of a
 // large body would hold up the whole launch)
@@ -146,7 +166,8 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
     const rpgpu_batch_result* __restrict__ vres, uint64_t* __restrict__ slot, uint64_t* __restrict__ local,
     uint64_t* __restrict__ block_sum, uint64_t max_decoded, uint32_t* __restrict__ wcount,
-    uint32_t* __restrict__ wlist) {
+    uint32_t* __restrict__ wlist, uint32_t* __restrict__ sfirst, uint32_t* __restrict__ scount,
+    SplitPart* __restrict__ parts, uint32_t pcap) {
     __shared__ uint64_t wsum[kScanBlock / 64];
     const uint32_t i = blockIdx.x * kScanBlock + threadIdx.x;
     uint64_t sz = 0;
@@ -183,12 +204,45 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
     if (i < n) {
         slot[i] = over ? kOverCeiling : sz;
         local[i] = wbase + x - span;
-        // the wave decoders' batches: zstd list at wlist[0..), LZ list at wlist[n..)
+        // large batches: LZ4 frames / snappy-java bodies with a split plan go
+        // to the part decoders (LZ4 parts at parts[0..), snappy's at
+        // parts[pcap / 2..)); the rest to the wave decoders (zstd list at
+        // wlist[0..), LZ list at wlist[n..))
+        uint32_t sf = 0, sc = 0;
         if (!over && sz > kLaneMaxSlot && decomp_wanted(descs[i], vres[i])) {
             const uint32_t c = vres[i].codec;
-            if (c == 4) wlist[atomicAdd(wcount, 1u)] = i;
-            else if (c == 2 || c == 3) wlist[n + atomicAdd(wcount + 1, 1u)] = i;
+            if (c == 2 || c == 3) {
+                const uint8_t* b = data + descs[i].offset + kHeaderSize;
+                const uint64_t body = body_len(vres[i]);
+                auto none = [](uint32_t, uint32_t, uint64_t, uint64_t, uint64_t, uint64_t, uint32_t) {};
+                const uint32_t half = pcap / 2;
+                const uint32_t np = c == 3 ? rpcodec::lz4f_split(b, body, half, none)
+                                           : rpcodec::snappy_java_split(b, body, half, none);
+                if (np) {
+                    const uint32_t k0 = atomicAdd(wcount + (c == 3 ? 2 : 3), np);
+                    if (k0 + np <= half) {
+                        SplitPart* const pp = parts + (c == 3 ? 0 : half) + k0;
+                        auto put = [&](uint32_t k, uint32_t kind, uint64_t io, uint64_t il, uint64_t oo, uint64_t oc,
+                                       uint32_t h) {
+                            SplitPart t;
+                            t.batch = i, t.kind = kind, t.in_off = (uint32_t)io, t.in_len = (uint32_t)il;
+                            t.out_off = oo, t.out_cap = (uint32_t)oc, t.hdr = h;
+                            pp[k] = t;
+                        };
+                        if (c == 3) rpcodec::lz4f_split(b, body, half, put);
+                        else rpcodec::snappy_java_split(b, body, half, put);
+                        sf = (c == 3 ? 0 : half) + k0;
+                        sc = np;
+                    }
+                }
+            }
+            if (!sc) {
+                if (c == 4) wlist[atomicAdd(wcount, 1u)] = i;
+                else if (c == 2 || c == 3) wlist[n + atomicAdd(wcount + 1, 1u)] = i;
+            }
         }
+        sfirst[i] = sf;
+        scount[i] = sc;
     }
     if (threadIdx.x == kScanBlock - 1) {
         uint64_t tot = 0;
@@ -427,6 +481,60 @@ __global__ __launch_bounds__(64) void decomp_wave_kernel(
     }
 }
 
+// The parts of split batches, one lane each (CODEC 3: LZ4 blocks, 2: snappy
+// chunks); every part writes only its own output range, so they run in any
+// order.  A batch whose slot does not fit the caller's buffer decodes nothing.
+template <uint32_t CODEC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_WAVES))) void part_kernel(
+    const SplitPart* __restrict__ parts, const uint32_t* __restrict__ pcount, uint32_t pcap,
+    const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data, const uint64_t* __restrict__ slot,
+    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base, uint8_t* __restrict__ out,
+    uint64_t out_cap, int32_t* __restrict__ pres) {
+    const uint32_t half = pcap / 2, base = CODEC == 3 ? 0 : half;
+    const uint32_t cnt = *pcount < half ? *pcount : half;
+    const uint32_t lanes = gridDim.x * blockDim.x;
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < cnt; g += lanes) {
+        const SplitPart t = parts[base + g];
+        const uint64_t off = block_base[t.batch / kScanBlock] + local[t.batch];
+        int32_t r = -2;
+        if (off + slot[t.batch] <= out_cap) {
+            const uint8_t* in = data + descs[t.batch].offset + kHeaderSize + t.in_off;
+            r = (int32_t)rpcodec::decode_part(t.kind, in, t.in_len, out + off + kHeaderSize + t.out_off, t.out_cap, t.hdr);
+        }
+        pres[base + g] = r;
+    }
+}
+
+// A split batch's verdict from its parts (rpcodec::split_result): decoded as
+// planned -> finished here; otherwise it joins the LZ wave list and is decoded
+// serially (the wave kernels run after this on the same stream).
+__global__ __launch_bounds__(256) void split_finish_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
+    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
+    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
+    const uint32_t* __restrict__ sfirst, const uint32_t* __restrict__ scount, const int32_t* __restrict__ pres,
+    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
+    rpgpu_batch_desc* __restrict__ out_descs, uint32_t* __restrict__ lz_count, uint32_t* __restrict__ wlist) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || scount[i] == 0) return;
+    const rpgpu_batch_desc d = descs[i];
+    const rpgpu_batch_result v = vres[i];
+    uint64_t sz = slot[i];
+    const uint64_t off = block_base[i / kScanBlock] + local[i];
+    int32_t verdict = RPGPU_V_OK;
+    uint64_t len = 0;
+    if (!plan_slot(sz, off, out_cap, verdict)) {
+        finish_batch(i, d, v, off, sz, verdict, 0, data, out, dres, out_descs);
+        return;
+    }
+    const uint32_t f = sfirst[i];
+    if (rpcodec::split_result(v.codec, data + d.offset + kHeaderSize, body_len(v), scount[i],
+                              [&](uint32_t k) { return (int64_t)pres[f + k]; }, &len))
+        finish_batch(i, d, v, off, sz, RPGPU_V_OK, len, data, out, dres, out_descs);
+    else
+        wlist[n + atomicAdd(lz_count, 1u)] = i;
+}
+
 // stores the CRCs the validation of the rewritten batches computed
 __global__ __launch_bounds__(256) void decomp_patch_kernel(const rpgpu_decomp_result* __restrict__ dres,
                                                            const rpgpu_batch_result* __restrict__ vres2, uint32_t n,
@@ -481,9 +589,11 @@ hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // wave-owned batch lists (filled by decomp_caps_kernel): counters 2 and 3
-    if ((e = hipMemsetAsync(p.counter + 2, 0, 2 * sizeof(uint32_t), s)) != hipSuccess) return e;
+    // counters 2, 3: wave list lengths; 4, 5: LZ4 / snappy parts
+    if ((e = hipMemsetAsync(p.counter + 2, 0, 4 * sizeof(uint32_t), s)) != hipSuccess) return e;
     decomp_caps_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
-                                                 max_decoded, p.counter + 2, p.wlist);
+                                                 max_decoded, p.counter + 2, p.wlist, p.sfirst, p.scount, p.parts,
+                                                 part_cap(n));
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_block_scan(p.block_sum, nb, d_out_bytes, s);
@@ -507,6 +617,16 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
         if ((e = hipStreamWaitEvent(ds->aux, ds->fork, 0)) != hipSuccess) return e;
         ws = ds->aux;
     }
+    // split batches: parts, then their verdicts (failures join the LZ wave list)
+    const uint32_t pgrid = (part_cap(n) / 2 < 65536u ? part_cap(n) / 2 + 255 : 65536u + 255) / 256;
+    part_kernel<3><<<pgrid, 256, 0, ws>>>(p.parts, p.counter + 4, part_cap(n), d_descs, d_data, p.slot, p.local,
+                                          p.block_sum, d_out, out_cap, p.pres);
+    part_kernel<2><<<pgrid, 256, 0, ws>>>(p.parts, p.counter + 5, part_cap(n), d_descs, d_data, p.slot, p.local,
+                                          p.block_sum, d_out, out_cap, p.pres);
+    split_finish_kernel<<<nblk, 256, 0, ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, p.sfirst,
+                                              p.scount, p.pres, d_dres, d_out, out_cap, d_out_descs, p.counter + 3,
+                                              p.wlist);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     decomp_wave_kernel<kFamZstd><<<decomp_waves(n), 64, sizeof(rpzstd::Ws), ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
                                                                 p.block_sum, d_dres, d_out, out_cap, d_out_descs,
                                                                 p.counter + 1, p.lits, p.wlist, p.counter + 2);

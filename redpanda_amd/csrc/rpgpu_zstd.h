@@ -116,26 +116,7 @@ RPC_HD uint64_t lomask(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1);
 // Unlike rpcodec's wild copies these write exactly n bytes: the Huffman
 // literals sit in the slot tail right behind the output, so no store may run
 // past the end of a sequence.
-RPC_HD void st_part(uint8_t* p, uint64_t lo, uint64_t hi, uint64_t n) {  // n < 16 bytes of lo|hi
-    if (n & 8) {
-        __builtin_memcpy(p, &lo, 8);
-        p += 8;
-        lo = hi;
-    }
-    if (n & 4) {
-        const uint32_t v = (uint32_t)lo;
-        __builtin_memcpy(p, &v, 4);
-        p += 4;
-        lo >>= 32;
-    }
-    if (n & 2) {
-        const uint16_t v = (uint16_t)lo;
-        __builtin_memcpy(p, &v, 2);
-        p += 2;
-        lo >>= 16;
-    }
-    if (n & 1) *p = (uint8_t)lo;
-}
+using rpcodec::st_part;  // n < 16 bytes of lo|hi
 // literals: src >= dst or disjoint (a forward copy whose 16-byte chunks are
 // each read before written; the last, overlapping chunk is read up front)
 RPC_HD void copy_lits(uint8_t* dst, const uint8_t* src, uint64_t n) {

@@ -34,7 +34,7 @@ namespace {
 typedef std::vector<uint8_t> Bytes;
 std::mt19937_64 rng;
 uint64_t below(uint64_t n) { return n ? rng() % n : 0; }
-long n_cases = 0, n_ok = 0, n_rejected = 0;
+long n_cases = 0, n_ok = 0, n_rejected = 0, n_split = 0, n_split_ok = 0;
 const uint8_t kEmpty[1] = {0};
 
 const uint8_t* ptr(const Bytes& b) { return b.empty() ? kEmpty : b.data(); }
@@ -354,6 +354,42 @@ void check(int codec, const Bytes& in, const char* what, long id) {
             exit(1);
         }
     }
+    // split plans (large LZ4 frames / snappy-java bodies decoded one part per
+    // lane): parts decoded in reverse order into one buffer (an overshoot
+    // into a later part would corrupt it), then the combined verdict; a plan
+    // that claims OK must reproduce the serial decode exactly
+    if (codec == 2 || codec == 3) {
+        struct Part {
+            uint32_t kind, hdr;
+            uint64_t in_off, in_len, out_off, out_cap;
+        };
+        std::vector<Part> parts;
+        auto add = [&](uint32_t, uint32_t kind, uint64_t io, uint64_t il, uint64_t oo, uint64_t oc, uint32_t h) {
+            parts.push_back(Part{kind, h, io, il, oo, oc});
+        };
+        const uint32_t np = codec == 3 ? rpcodec::lz4f_split(ib.data(), n, 1u << 20, add)
+                                       : rpcodec::snappy_java_split(ib.data(), n, 1u << 20, add);
+        if (np) {
+            n_split++;
+            const uint64_t tot = parts.back().out_off + parts.back().out_cap;
+            Bytes pb(tot + 64, 0x5A);
+            std::vector<int64_t> res(np);
+            for (uint32_t k = np; k-- > 0;)
+                res[k] = rpcodec::decode_part(parts[k].kind, ib.data() + parts[k].in_off, parts[k].in_len,
+                                              pb.data() + parts[k].out_off, parts[k].out_cap, parts[k].hdr);
+            uint64_t plen = 0;
+            const bool pok = rpcodec::split_result((uint32_t)codec, ib.data(), n, np,
+                                                   [&](uint32_t k) { return res[k]; }, &plen);
+            bool bad = pok && (gv != 0 || plen != glen || (glen && memcmp(pb.data(), ob.data(), glen)));
+            for (uint64_t k = tot; !bad && k < tot + 64; k++) bad = pb[k] != 0x5A;
+            if (bad) {
+                fprintf(stderr, "SPLIT DIVERGENCE case %ld (%s) codec %d: serial %d len %llu, split ok %d len %llu\n", id,
+                        what, codec, gv, (unsigned long long)glen, (int)pok, (unsigned long long)plen);
+                exit(1);
+            }
+            if (pok) n_split_ok++;
+        }
+    }
     const size_t ocap = bound + (1u << 20);
     Bytes rb(ocap);
     size_t rlen = 0;
@@ -442,6 +478,7 @@ int main(int argc, char** argv) {
             check(below(2) ? 2 : 3, g, "garbage", c);
         }
     }
-    printf("codec fuzz: %ld cases, %ld decoded, %ld rejected: engine == oracle\n", n_cases, n_ok, n_rejected);
+    printf("codec fuzz: %ld cases, %ld decoded, %ld rejected, %ld split plans (%ld taken): engine == oracle\n", n_cases,
+           n_ok, n_rejected, n_split, n_split_ok);
     return 0;
 }
