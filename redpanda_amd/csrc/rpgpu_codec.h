@@ -466,7 +466,7 @@ RPC_HD int64_t lz4_block(E& em, const uint8_t* in, int64_t isz, uint8_t* out, in
 // store); this form spends one:
 //   - tokens, lengths and offsets are read from a 64-byte register window
 //     whose next 32 bytes are prefetched a step ahead;
-//   - a sequence with <= 32 literal bytes and a match of <= 48 bytes whose
+//   - a sequence with <= 32 literal bytes and a match of <= 32 bytes whose
 //     source lies before it (offset >= 16 per 16-byte chunk), or any match
 //     with offset < 16 (a period rebuilt in registers), issues all its loads
 //     at once -- literal bytes, the match source's chunks -- and composes the
@@ -586,7 +586,14 @@ RPC_HD uint32_t lz4_varlen64(Win64& W, const uint8_t* in, int32_t& ip, int32_t l
 
 // Returns the decoded size, or -1 (lz4_block's contract).  `lim` = bytes of
 // `in` that may be read (the block plus the arena's tail padding).
-RPC_HD int32_t lz4_block_lane(const uint8_t* in, int32_t isz, uint8_t* out, int32_t ocap, int32_t hist,
+// Out of line on the device: the frame loop's state stays out of the
+// sequence loop's registers (128 VGPRs at 4 waves per SIMD).
+#ifdef __HIPCC__
+static __host__ __device__ __attribute__((noinline))
+#else
+static inline
+#endif
+int32_t lz4_block_lane(const uint8_t* in, int32_t isz, uint8_t* out, int32_t ocap, int32_t hist,
                               int32_t lim) {
     if (isz == 0) return -1;
     const int32_t iend = isz, oend = ocap;
@@ -664,7 +671,7 @@ RPC_HD int32_t lz4_block_lane(const uint8_t* in, int32_t isz, uint8_t* out, int3
         // ---- copies
         const bool pat = off < 16;
         const int32_t nch = pat ? 1 : (ml + 15) >> 4;
-        if (last || ll > 32 || (!pat && (ml > 48 || off < 16 * nch)) || op_m + ml + 15 > oend) {
+        if (last || ll > 32 || (!pat && (ml > 32 || off < 16 * nch)) || op_m + ml + 15 > oend) {
             // exact copies: nothing is written past the block's capacity
             // (a split frame's next block may already be there)
             if (ll) copy_exact(out + op, in + ip_lit, (uint64_t)ll);
@@ -676,23 +683,22 @@ RPC_HD int32_t lz4_block_lane(const uint8_t* in, int32_t isz, uint8_t* out, int3
         // one round trip: every load of the sequence, then its stores
         const int32_t rel = ll - off;  // match source start - literal start
         const uint8_t* src = out + op_m - off;
-        V16 L0{0, 0}, L1{0, 0}, A0{0, 0}, A1{0, 0}, A2{0, 0};
+        V16 L0{0, 0}, L1{0, 0}, A0{0, 0}, A1{0, 0};
         if (ll > 0) L0 = v16_ld(in + ip_lit);
         if (ll > 16) L1 = v16_ld(in + ip_lit + 16);
         if (off != 0 && rel < 0) A0 = v16_ld(src);
         if (!pat && nch > 1 && rel + 16 < 0) A1 = v16_ld(src + 16);
-        if (!pat && nch > 2 && rel + 32 < 0) A2 = v16_ld(src + 32);
-        if (ll > 0) v16_st(out + op, L0);
-        if (ll > 16) v16_st(out + op + 16, L1);
         // 16 source bytes at literal-relative r: stored bytes (A) below the
         // literal run, the run's own bytes (registers) from it on
-        const int32_t r0 = rel, r1 = rel + 16, r2 = rel + 32;
+        const int32_t r0 = rel, r1 = rel + 16;
         const V16 c0 = r0 >= 0 ? v16_ext(L0, L1, (uint32_t)r0)
                        : r0 <= -16 ? A0 : v16_merge(A0, v16_shl(L0, (uint32_t)-r0), (uint32_t)-r0);
+        V16 first = c0;  // the match's first 16 bytes
+        uint64_t step = 16;
         if (pat) {
             // period-off pattern (off 0: liblz4's zeros), stored a whole
             // number of periods apart
-            uint64_t lo = 0, hi = 0, step = 16;
+            uint64_t lo = 0, hi = 0;
             if (off != 0) {
                 lo = c0.lo;
                 hi = c0.hi;
@@ -713,19 +719,23 @@ RPC_HD int32_t lz4_block_lane(const uint8_t* in, int32_t isz, uint8_t* out, int3
                 }
                 step = (uint64_t)off * (16 / (uint64_t)off);
             }
-            const V16 pv{lo, hi};
-            for (uint64_t i = 0; i < (uint64_t)ml; i += step) v16_st(out + op_m + i, pv);
+            first = V16{lo, hi};
+        }
+        if (ll + ml <= 16) {
+            // the whole sequence in one 16-byte store (most text sequences)
+            v16_st(out + op, ll ? v16_merge(L0, v16_shl(first, (uint32_t)ll), (uint32_t)ll) : first);
         } else {
-            v16_st(out + op_m, c0);
-            if (nch > 1) {
-                const V16 c1 = r1 >= 0 ? v16_ext(L0, L1, (uint32_t)r1)
-                               : r1 <= -16 ? A1 : v16_merge(A1, v16_shl(L0, (uint32_t)-r1), (uint32_t)-r1);
-                v16_st(out + op_m + 16, c1);
-            }
-            if (nch > 2) {
-                const V16 c2 = r2 >= 0 ? v16_ext(L0, L1, (uint32_t)r2)
-                               : r2 <= -16 ? A2 : v16_merge(A2, v16_shl(L0, (uint32_t)-r2), (uint32_t)-r2);
-                v16_st(out + op_m + 32, c2);
+            if (ll > 0) v16_st(out + op, L0);
+            if (ll > 16) v16_st(out + op + 16, L1);
+            if (pat) {
+                for (uint64_t i = 0; i < (uint64_t)ml; i += step) v16_st(out + op_m + i, first);
+            } else {
+                v16_st(out + op_m, c0);
+                if (nch > 1) {
+                    const V16 c1 = r1 >= 0 ? v16_ext(L0, L1, (uint32_t)r1)
+                                   : r1 <= -16 ? A1 : v16_merge(A1, v16_shl(L0, (uint32_t)-r1), (uint32_t)-r1);
+                    v16_st(out + op_m + 16, c1);
+                }
             }
         }
         op = op_m + ml;
