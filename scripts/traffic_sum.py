@@ -1,0 +1,51 @@
+"""Per-launch HBM traffic of a decompress pipeline from rocprofv3 PMC passes
+(scripts/gpu_pmc_traffic.sh with --steps 1 --warmup 0): FETCH_SIZE and
+WRITE_SIZE (KB, summed over the device) of every rpgpu:: kernel dispatch of
+the one timed step, merged into profiles/traffic.json under the config.
+
+FETCH_SIZE is reported raw: the decoders' reads are scattered 16-byte
+accesses, for which MI355X_MICROARCH.md's 2x streaming-read correction is
+uncalibrated; validate_kernel's streaming reads are doubled as the guide
+prescribes.  usage: traffic_sum.py <pmc dir> <config> <batches>"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+root, cfg, nb = sys.argv[1], sys.argv[2], int(sys.argv[3])
+# mean per dispatch of each kernel, times its launches per pipeline step (the
+# validation and the walk run twice: over the compressed and the rewritten
+# batches; the run may hold extra dispatches outside the step)
+tot = defaultdict(lambda: defaultdict(float))
+disp = defaultdict(lambda: defaultdict(set))
+for f in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True)):
+    for row in csv.DictReader(open(f)):
+        k = row.get("Kernel_Name", "")
+        if "rpgpu::" not in k:
+            continue
+        name = k.split("(")[0]
+        tot[row["Counter_Name"]][name] += float(row["Counter_Value"])
+        disp[row["Counter_Name"]][name].add(row["Dispatch_Id"])
+per = defaultdict(dict)
+for c in tot:
+    for name, v in tot[c].items():
+        calls = 2 if ("validate_kernel" in name or "walk_kernel" in name) else 1
+        per[c][name] = v / len(disp[c][name]) * calls
+fetch = sum(v * (2.0 if "validate_kernel" in k else 1.0) for k, v in per["FETCH_SIZE"].items()) * 1024
+write = sum(per["WRITE_SIZE"].values()) * 1024
+out = {"batches": nb,
+       "kernel": "every rpgpu:: kernel of one pipeline step",
+       "fetch_bytes": int(fetch), "write_bytes": int(write),
+       "hbm_bytes_per_launch": int(fetch + write),
+       "raw_counters_kb_per_step": {c: dict(v) for c, v in per.items()},
+       "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / TCC_HIT_sum TCC_MISS_sum in separate passes "
+                 "(scripts/gpu_pmc_traffic.sh, --steps 1 --warmup 0); validate_kernel FETCH doubled "
+                 "(16-B/lane streaming reads, MI355X_MICROARCH.md); the decoders' scattered reads raw"}
+p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic.json")
+doc = json.load(open(p)) if os.path.exists(p) else {}
+doc[cfg] = out
+json.dump(doc, open(p, "w"), indent=1)
+sums = {c: sum(v.values()) for c, v in per.items()}
+print(cfg, "fetch GB", round(fetch / 1e9, 2), "write GB", round(write / 1e9, 2), {k: f"{v:.3g}" for k, v in sums.items()})
