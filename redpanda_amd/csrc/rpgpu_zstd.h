@@ -82,6 +82,11 @@ constexpr uint64_t kUnknown = ~0ull;                  // ZSTD_CONTENTSIZE_UNKNOW
 // ZSTD_estimateDStreamSize(8 MiB) - sizeof(ZSTD_DCtx): in 128 KiB + out 8 MiB + 128 KiB + 64
 constexpr uint64_t kBudget = 131072u + 8388608u + 131072u + 64u;
 constexpr uint32_t kHufMaxLog = 12;                   // HufLog: the DCtx's Huffman table
+// First-level Huffman table for workspaces in HBM: 256 entries (512 B, cache-resident
+// across a lane's symbols) that resolve every code of <= 8 bits; longer codes fall
+// through to the full table.  Same symbols and bit counts as the full table.
+constexpr uint32_t kHuf1Log = 8;
+constexpr uint16_t kHuf1None = 0xFFFF;
 
 // ------------------------------------------------------------------ tables
 // Sequence codes -> (baseline, extra bits) (zstd_decompress_block.c LL_base /
@@ -251,6 +256,7 @@ RPC_HD bool huf_select_x2(uint64_t dst, uint64_t csrc) {
 // Per-frame decoder state (per lane in HBM on the device; LDS for the scalar mirror): ~19 KB.
 struct Ws {
     uint16_t huf[1u << kHufMaxLog];  // X1 table: symbol | nbBits << 8
+    uint16_t huf1[1u << kHuf1Log];   // huf by the first kHuf1Log bits where that decides the code, else kHuf1None
     uint32_t ll[512], ml[512], of[256];  // sequence tables: state << 16 | nbBits << 8 | symbol
     uint32_t llx[512], mlx[512];     // per state: baseline | extra bits << 24 (ZSTD_seqSymbol's
                                      // baseValue / nbAdditionalBits: no dependent lookup per field)
@@ -261,7 +267,7 @@ struct Ws {
     uint32_t rank[kHufMaxLog + 1];
     uint64_t rep[3];
     uint8_t ll_log, ml_log, of_log, huf_log;
-    uint8_t huf_x2, lit_entropy, fse_entropy, pad;
+    uint8_t huf_x2, lit_entropy, fse_entropy, huf1_on;
 #if RPZ_PROF
     uint64_t t_lit, t_seq, n_seq, n_lit;  // diagnostics build: clock64 per phase
 #endif
@@ -579,6 +585,12 @@ RPC_HD int64_t huf_read_table(Ws& w, const uint8_t* in, uint64_t n) {
         w.rank[wt] += len;
     }
     w.huf_log = (uint8_t)log;
+    w.huf1_on = log > kHuf1Log;
+    if (w.huf1_on)
+        for (uint32_t i = 0; i < (1u << kHuf1Log); i++) {
+            const uint16_t e = w.huf[i << (log - kHuf1Log)];
+            w.huf1[i] = (e >> 8) <= kHuf1Log ? e : kHuf1None;
+        }
     return (int64_t)iSize + 1;
 }
 
@@ -617,7 +629,15 @@ RPC_HD void huf_end(HufS& h) {
 #endif
     h.ok = h.ok && h.b.pos == 0;
 }
-RPC_HD void huf_step(const Ws& w, HufS& h, uint32_t L, bool x2) {
+// the X1 entry of the L-bit index v (two: through huf1 first)
+RPC_HD uint32_t huf_entry(const Ws& w, uint32_t v, uint32_t L, bool two) {
+    if (two) {
+        const uint32_t t = w.huf1[v >> (L - kHuf1Log)];
+        if (t != kHuf1None) return t;
+    }
+    return w.huf[v];
+}
+RPC_HD void huf_step(const Ws& w, HufS& h, uint32_t L, bool x2, bool two = false) {
     if (!h.live) return;
     if (h.b.pos < 0) {
         h.ok = false;
@@ -628,9 +648,9 @@ RPC_HD void huf_step(const Ws& w, HufS& h, uint32_t L, bool x2) {
     if (x2 && !h.second) {
         // the X2 entry: the 12-bit window holds this code and, if it fits, the next
         const uint32_t v = peek_fast(h.b, h.b.pos, kHufMaxLog);
-        const uint32_t e = w.huf[v >> (kHufMaxLog - L)];
+        const uint32_t e = huf_entry(w, v >> (kHufMaxLog - L), L, two);
         const uint32_t nb = e >> 8;
-        const uint32_t e2 = w.huf[((v << nb) & ((1u << kHufMaxLog) - 1)) >> (kHufMaxLog - L)];
+        const uint32_t e2 = huf_entry(w, ((v << nb) & ((1u << kHufMaxLog) - 1)) >> (kHufMaxLog - L), L, two);
         const bool pair = nb + (e2 >> 8) <= kHufMaxLog;
         if (i < h.nwrite) bo_put(h.o, e);
         if (i + 1 == h.nsym) {  // HUF_decodeLastSymbolX2
@@ -646,7 +666,7 @@ RPC_HD void huf_step(const Ws& w, HufS& h, uint32_t L, bool x2) {
         h.second = pair;
         h.b.pos -= nb;
     } else {
-        const uint32_t e = w.huf[peek_fast(h.b, h.b.pos, L)];
+        const uint32_t e = huf_entry(w, peek_fast(h.b, h.b.pos, L), L, two);
         if (i < h.nwrite) bo_put(h.o, e);
         h.second = false;
         h.b.pos -= e >> 8;
@@ -654,13 +674,14 @@ RPC_HD void huf_step(const Ws& w, HufS& h, uint32_t L, bool x2) {
     h.i = i + 1;
     if (h.i == h.nsym) huf_end(h);
 }
-RPC_HD bool huf_stream(const Ws& w, const uint8_t* src, uint64_t len, uint8_t* out, uint64_t nsym, uint64_t nwrite) {
+RPC_HD bool huf_stream(const Ws& w, const uint8_t* src, uint64_t len, uint8_t* out, uint64_t nsym, uint64_t nwrite,
+                       bool two = false) {
     HufS h;
     if (!huf_begin(h, src, len, out, nsym, nwrite)) return RPZ_FAIL(false);
     if (!h.live) huf_end(h);
     const uint32_t L = w.huf_log;
     const bool x2 = w.huf_x2 != 0;
-    while (h.live) huf_step(w, h, L, x2);
+    while (h.live) huf_step(w, h, L, x2, two);
     return h.ok;
 }
 
@@ -696,11 +717,12 @@ struct DirectEmit {
     RPC_HD uint8_t* litbuf(uint8_t* out, uint64_t tail, uint64_t size) { return out + tail - size; }
     RPC_HD void litfill(uint8_t* d, uint8_t v, uint64_t n) { fill_bytes(d, v, n); }
     RPC_HD bool huf1(const Ws& w, const uint8_t* src, uint64_t len, uint8_t* d, uint64_t n) {
-        return huf_stream(w, src, len, d, n, n);
+        return huf_stream(w, src, len, d, n, n, w.huf1_on != 0);  // Ws in HBM: the first-level table
     }
     RPC_HD bool huf4(const Ws& w, const Huf4& a) {
         const uint32_t L = w.huf_log;
         const bool x2 = w.huf_x2 != 0;
+        const bool two = w.huf1_on != 0;  // Ws in HBM: the first-level table
         HufS h0, h1, h2, h3;
         huf_begin(h0, a.s[0], a.len[0], a.d[0], a.nsym[0], a.nwrite[0]);
         huf_begin(h1, a.s[1], a.len[1], a.d[1], a.nsym[1], a.nwrite[1]);
@@ -711,10 +733,10 @@ struct DirectEmit {
         if (!h2.live) huf_end(h2);
         if (!h3.live) huf_end(h3);
         while (h0.live | h1.live | h2.live | h3.live) {
-            huf_step(w, h0, L, x2);
-            huf_step(w, h1, L, x2);
-            huf_step(w, h2, L, x2);
-            huf_step(w, h3, L, x2);
+            huf_step(w, h0, L, x2, two);
+            huf_step(w, h1, L, x2, two);
+            huf_step(w, h2, L, x2, two);
+            huf_step(w, h3, L, x2, two);
         }
         return h0.ok && h1.ok && h2.ok && h3.ok;
     }
@@ -859,9 +881,13 @@ RPC_HD void seq_extra(Ws& w, uint32_t which) {
     }
 }
 RPC_HD int64_t seq_table_impl(Ws& w, uint32_t mode, uint32_t which, const uint8_t* in, uint64_t n);
-RPC_HD int64_t seq_table(Ws& w, uint32_t mode, uint32_t which, const uint8_t* in, uint64_t n) {
+// extra: also fill the per-state baseline tables (llx / mlx) -- for workspaces
+// in LDS, where they save a dependent lookup; a workspace in HBM reads the
+// baselines from the 89-entry code tables instead (one cached line, not a
+// line of HBM per sequence)
+RPC_HD int64_t seq_table(Ws& w, uint32_t mode, uint32_t which, const uint8_t* in, uint64_t n, bool extra) {
     const int64_t h = seq_table_impl(w, mode, which, in, n);
-    if (h >= 0 && mode != 3) seq_extra(w, which);
+    if (extra && h >= 0 && mode != 3) seq_extra(w, which);
     return h;
 }
 RPC_HD int64_t seq_table_impl(Ws& w, uint32_t mode, uint32_t which, const uint8_t* in, uint64_t n) {
@@ -903,6 +929,7 @@ template <class E>
 RPZ_COLD int64_t block(E& em, Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t fstart, uint64_t op,
                        uint64_t cap, uint64_t tail) {
     if (n >= kBlockMax) return RPZ_FAIL(-1);
+    constexpr bool kLdsWs = E::kInlineBlocks;  // the wave decoders keep Ws in LDS
     Lit lit;
 #if RPZ_PROF
     const uint64_t c0 = RPZ_CLK();
@@ -936,13 +963,13 @@ RPZ_COLD int64_t block(E& em, Ws& w, const uint8_t* in, uint64_t n, uint8_t* out
         }
         if (p + 1 > iend) return RPZ_FAIL(-1);
         const uint32_t modes = *p++;
-        int64_t h = seq_table(w, modes >> 6, 0, p, (uint64_t)(iend - p));
+        int64_t h = seq_table(w, modes >> 6, 0, p, (uint64_t)(iend - p), kLdsWs);
         if (h < 0) return RPZ_FAIL(-1);
         p += h;
-        h = seq_table(w, (modes >> 4) & 3, 1, p, (uint64_t)(iend - p));
+        h = seq_table(w, (modes >> 4) & 3, 1, p, (uint64_t)(iend - p), kLdsWs);
         if (h < 0) return RPZ_FAIL(-1);
         p += h;
-        h = seq_table(w, (modes >> 2) & 3, 2, p, (uint64_t)(iend - p));
+        h = seq_table(w, (modes >> 2) & 3, 2, p, (uint64_t)(iend - p), kLdsWs);
         if (h < 0) return RPZ_FAIL(-1);
         p += h;
     }
@@ -960,7 +987,9 @@ RPZ_COLD int64_t block(E& em, Ws& w, const uint8_t* in, uint64_t n, uint8_t* out
         uint32_t sML = (uint32_t)read_bits(b, w.ml_log);
         for (uint32_t k = 0; k < nbSeq; k++) {
             const uint32_t eLL = w.ll[sLL], eML = w.ml[sML], eOF = w.of[sOF];
-            const uint32_t xLL = w.llx[sLL], xML = w.mlx[sML];
+            const uint32_t cLL = eLL & 0xFF, cML = eML & 0xFF;  // <= 35 / 52: FSE symbols are checked
+            const uint32_t xLL = kLdsWs ? w.llx[sLL] : (kLLBase[cLL] | ((uint32_t)kLLBits[cLL] << 24));
+            const uint32_t xML = kLdsWs ? w.mlx[sML] : (kMLBase[cML] | ((uint32_t)kMLBits[cML] << 24));
             const uint32_t cOF = eOF & 0xFF;
             const uint32_t llBase = xLL & 0xFFFFFF, mlBase = xML & 0xFFFFFF;
             const uint32_t llBits = xLL >> 24, mlBits = xML >> 24, ofBits = cOF;
