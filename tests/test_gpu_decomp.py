@@ -147,6 +147,35 @@ def test_large_bodies(eng):
     compare(eng.decompress_arena(data, descs), data, descs)
 
 
+def test_large_bodies_split_fallback(eng):
+    """~1 MiB LZ4 frames (independent 64 KiB blocks) and snappy-java bodies
+    (128 KiB chunks) decoded one part per lane (rpcodec::lz4f_split /
+    snappy_java_split), clean and damaged so that a part fails (a flipped or
+    0xFF byte inside a block / chunk: the batch goes back to the serial
+    decoder) or no plan is made (cut short, trailing junk): every verdict,
+    length and byte as the oracle's."""
+    rng = np.random.default_rng(11)
+    bs = []
+    for codec in (3, 2):
+        for kind in range(6):
+            recs = records(rng, 900, 8, 1100, text=True)
+            comp = bytearray(orc.compress(codec, b"".join(recs)))
+            n = len(comp)
+            if kind == 1:
+                comp[n // 2] ^= 0x5A
+            elif kind == 2:
+                comp[n - 40] ^= 0x01
+            elif kind == 3:
+                comp = comp[: int(n * 0.6)]
+            elif kind == 4:
+                comp += b"\x00junk"
+            elif kind == 5:
+                comp[n // 3] = 0xFF
+            bs.append(batch(bytes(comp), fmt=WIRE, record_count=len(recs), attrs=codec))
+    data, descs = arena(bs, fmt=WIRE, ops=OPS)
+    compare(eng.decompress_arena(data, descs), data, descs)
+
+
 def test_uncompress_scalar_mirror(eng):
     rng = np.random.default_rng(3)
     cases = []
