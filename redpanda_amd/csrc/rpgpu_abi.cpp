@@ -216,7 +216,8 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
     c->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     c->have_dstreams = hipStreamCreateWithFlags(&c->dstreams.aux, hipStreamNonBlocking) == hipSuccess &&
                        hipEventCreateWithFlags(&c->dstreams.fork, hipEventDisableTiming) == hipSuccess &&
-                       hipEventCreateWithFlags(&c->dstreams.join, hipEventDisableTiming) == hipSuccess;
+                       hipEventCreateWithFlags(&c->dstreams.join, hipEventDisableTiming) == hipSuccess &&
+                       hipEventCreateWithFlags(&c->dstreams.parts, hipEventDisableTiming) == hipSuccess;
     c->have_overlap = hipStreamCreateWithFlags(&c->overlap.aux, hipStreamNonBlocking) == hipSuccess;
     for (int k = 0; c->have_overlap && k <= c->overlap.chunks; k++)
         c->have_overlap = hipEventCreateWithFlags(&c->overlap.ev[k], hipEventDisableTiming) == hipSuccess;
@@ -260,6 +261,7 @@ void rpgpu_close(rpgpu_ctx* c) {
     }
     if (c->dstreams.fork) (void)hipEventDestroy(c->dstreams.fork);
     if (c->dstreams.join) (void)hipEventDestroy(c->dstreams.join);
+    if (c->dstreams.parts) (void)hipEventDestroy(c->dstreams.parts);
     delete c;
 }
 

@@ -617,19 +617,27 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
         if ((e = hipStreamWaitEvent(ds->aux, ds->fork, 0)) != hipSuccess) return e;
         ws = ds->aux;
     }
-    // split batches: parts, then their verdicts (failures join the LZ wave list)
+    // split batches: LZ4 parts ahead of the lane kernels on the main stream,
+    // snappy parts on the second, then their verdicts there (failures join
+    // the LZ wave list); the two streams' chains come out about even
     const uint32_t pgrid = (part_cap(n) / 2 < 65536u ? part_cap(n) / 2 + 255 : 65536u + 255) / 256;
-    part_kernel<3><<<pgrid, 256, 0, ws>>>(p.parts, p.counter + 4, part_cap(n), d_descs, d_data, p.slot, p.local,
-                                          p.block_sum, d_out, out_cap, p.pres);
-    part_kernel<2><<<pgrid, 256, 0, ws>>>(p.parts, p.counter + 5, part_cap(n), d_descs, d_data, p.slot, p.local,
-                                          p.block_sum, d_out, out_cap, p.pres);
-    split_finish_kernel<<<nblk, 256, 0, ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, p.sfirst,
-                                              p.scount, p.pres, d_dres, d_out, out_cap, d_out_descs, p.counter + 3,
-                                              p.wlist);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    part_kernel<3><<<pgrid, 256, 0, s>>>(p.parts, p.counter + 4, part_cap(n), d_descs, d_data, p.slot, p.local,
+                                         p.block_sum, d_out, out_cap, p.pres);
+    if (ds) {
+        if ((e = hipEventRecord(ds->parts, s)) != hipSuccess) return e;
+    }
+    // the zstd wave decoder first on the second stream: it does not wait for the parts
     decomp_wave_kernel<kFamZstd><<<decomp_waves(n), 64, sizeof(rpzstd::Ws), ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
                                                                 p.block_sum, d_dres, d_out, out_cap, d_out_descs,
                                                                 p.counter + 1, p.lits, p.wlist, p.counter + 2);
+    part_kernel<2><<<pgrid, 256, 0, ws>>>(p.parts, p.counter + 5, part_cap(n), d_descs, d_data, p.slot, p.local,
+                                          p.block_sum, d_out, out_cap, p.pres);
+    if (ds) {
+        if ((e = hipStreamWaitEvent(ws, ds->parts, 0)) != hipSuccess) return e;
+    }
+    split_finish_kernel<<<nblk, 256, 0, ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, p.sfirst,
+                                              p.scount, p.pres, d_dres, d_out, out_cap, d_out_descs, p.counter + 3,
+                                              p.wlist);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     decomp_wave_kernel<kFamLz><<<decomp_waves(n), 64, 0, ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
                                                               p.block_sum, d_dres, d_out, out_cap, d_out_descs,

@@ -51,7 +51,7 @@ struct Overlap {
 // beside the lane decoders (fork / join events)
 struct DecompStreams {
     hipStream_t aux;
-    hipEvent_t fork, join;
+    hipEvent_t fork, join, parts;  // parts: the LZ4 part decoder (main stream) is done
 };
 
 void build_tables(uint32_t* out /* kTableWords */);
