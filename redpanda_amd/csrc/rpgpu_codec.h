@@ -1148,27 +1148,46 @@ RPC_HD int64_t decode_part(uint32_t kind, const uint8_t* in, uint64_t in_len, ui
     BoundEmit em{out + out_cap};
     return snappy_raw(em, in, in_len, out, (uint32_t)out_cap, hdr) ? (int64_t)out_cap : -1;
 }
-// The serial verdict of a planned body whose parts all decoded: OK and the
-// total length, or false (the body goes to the serial decoder).  r(k) = part
-// k's decoded size.
+// The serial decoder's verdict for a planned body from its parts' decoded
+// sizes r(k) (-1: the part is corrupt): V_OK or V_ERROR with *len as the serial
+// decoder leaves it, or kSplitSerial when only the serial decoder can tell (a
+// non-final LZ4 block decoded short: the serial decoder would place the next
+// block elsewhere).  The first corrupt part, in order, ends the serial decode:
+// an LZ4 block -> V_ERROR with no output (lz4f_uncompress: decompressionFailed;
+// independent blocks decode the same wherever they are placed), a snappy chunk
+// -> V_ERROR with the chunks before it (snappy_java_uncompress).
+constexpr int32_t kSplitSerial = -1;
 template <class R>
-RPC_HD bool split_result(uint32_t codec, const uint8_t* in, uint64_t n, uint32_t parts, R&& r, uint64_t* len) {
+RPC_HD int32_t split_result(uint32_t codec, const uint8_t* in, uint64_t n, uint32_t parts, R&& r, uint64_t* len) {
     uint64_t o = 0;
-    bool ok = true;
+    bool placed = true, bad = false;
     auto check = [&](uint32_t k, uint32_t kind, uint64_t, uint64_t, uint64_t out_off, uint64_t out_cap, uint32_t) {
+        if (bad) return;
         const int64_t d = r(k);
-        if (d < 0 || (kind == kPartLz4Block && k + 1 < parts && (uint64_t)d != out_cap)) ok = false;
-        o = out_off + (d < 0 ? 0 : (uint64_t)d);
+        if (d < 0) {
+            bad = true;
+            o = codec == 3 ? 0 : out_off;
+            return;
+        }
+        if (kind == kPartLz4Block && k + 1 < parts && (uint64_t)d != out_cap) placed = false;
+        o = out_off + (uint64_t)d;
     };
-    if (codec == 3) {
-        if (lz4f_split(in, n, parts, check) != parts) return false;
-        const Lz4Frame f = lz4f_header(in, n);
-        if (f.content != 0 && o != f.content) ok = false;  // frameSize_wrong: the serial decoder's verdict
-    } else {
-        if (snappy_java_split(in, n, parts, check) != parts) return false;
+    if ((codec == 3 ? lz4f_split(in, n, parts, check) : snappy_java_split(in, n, parts, check)) != parts)
+        return kSplitSerial;
+    if (bad) {
+        *len = o;
+        return V_ERROR;
     }
+    if (!placed) return kSplitSerial;
     *len = o;
-    return ok;
+    if (codec == 3) {
+        const Lz4Frame f = lz4f_header(in, n);
+        if (f.content != 0 && o != f.content) {  // frameSize_wrong
+            *len = 0;
+            return V_ERROR;
+        }
+    }
+    return V_OK;
 }
 
 // ---------------------------------------------------------------- dispatch

@@ -505,9 +505,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_
     }
 }
 
-// A split batch's verdict from its parts (rpcodec::split_result): decoded as
-// planned -> finished here; otherwise it joins the LZ wave list and is decoded
-// serially (the wave kernels run after this on the same stream).
+// A split batch's verdict from its parts (rpcodec::split_result): OK or a
+// corrupt part's error -> finished here; a plan the parts did not bear out
+// joins the LZ wave list and is decoded serially (the wave kernels run after
+// this on the same stream).
 __global__ __launch_bounds__(256) void split_finish_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
     const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
@@ -528,9 +529,10 @@ __global__ __launch_bounds__(256) void split_finish_kernel(
         return;
     }
     const uint32_t f = sfirst[i];
-    if (rpcodec::split_result(v.codec, data + d.offset + kHeaderSize, body_len(v), scount[i],
-                              [&](uint32_t k) { return (int64_t)pres[f + k]; }, &len))
-        finish_batch(i, d, v, off, sz, RPGPU_V_OK, len, data, out, dres, out_descs);
+    verdict = rpcodec::split_result(v.codec, data + d.offset + kHeaderSize, body_len(v), scount[i],
+                                    [&](uint32_t k) { return (int64_t)pres[f + k]; }, &len);
+    if (verdict != rpcodec::kSplitSerial)
+        finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
     else
         wlist[n + atomicAdd(lz_count, 1u)] = i;
 }

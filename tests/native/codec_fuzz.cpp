@@ -378,16 +378,19 @@ void check(int codec, const Bytes& in, const char* what, long id) {
                 res[k] = rpcodec::decode_part(parts[k].kind, ib.data() + parts[k].in_off, parts[k].in_len,
                                               pb.data() + parts[k].out_off, parts[k].out_cap, parts[k].hdr);
             uint64_t plen = 0;
-            const bool pok = rpcodec::split_result((uint32_t)codec, ib.data(), n, np,
-                                                   [&](uint32_t k) { return res[k]; }, &plen);
-            bool bad = pok && (gv != 0 || plen != glen || (glen && memcmp(pb.data(), ob.data(), glen)));
+            const int32_t sv = rpcodec::split_result((uint32_t)codec, ib.data(), n, np,
+                                                     [&](uint32_t k) { return res[k]; }, &plen);
+            const bool pok = sv == 0;
+            // a verdict from the parts must be the serial one (with its length); OK also its bytes
+            bool bad = sv != rpcodec::kSplitSerial &&
+                       (sv != gv || plen != glen || (pok && glen && memcmp(pb.data(), ob.data(), glen)));
             for (uint64_t k = tot; !bad && k < tot + 64; k++) bad = pb[k] != 0x5A;
             if (bad) {
-                fprintf(stderr, "SPLIT DIVERGENCE case %ld (%s) codec %d: serial %d len %llu, split ok %d len %llu\n", id,
-                        what, codec, gv, (unsigned long long)glen, (int)pok, (unsigned long long)plen);
+                fprintf(stderr, "SPLIT DIVERGENCE case %ld (%s) codec %d: serial %d len %llu, split %d len %llu\n", id,
+                        what, codec, gv, (unsigned long long)glen, sv, (unsigned long long)plen);
                 exit(1);
             }
-            if (pok) n_split_ok++;
+            if (sv != rpcodec::kSplitSerial) n_split_ok++;
         }
     }
     const size_t ocap = bound + (1u << 20);
