@@ -130,6 +130,11 @@ size_t decomp_scratch_bytes(uint32_t n) {
 // slots above this go to the wave decoders (a lane's serial decode of a
 // large body would hold up the whole launch)
 constexpr uint64_t kLaneMaxSlot = 256u << 10;
+#ifndef RPGPU_ZSTD_LANE_MAX
+#define RPGPU_ZSTD_LANE_MAX (256u << 10)
+#endif
+constexpr uint64_t kZstdLaneMaxSlot = RPGPU_ZSTD_LANE_MAX;  // zstd: its lane / wave boundary
+__device__ __forceinline__ uint64_t lane_max(uint32_t codec) { return codec == 4 ? kZstdLaneMaxSlot : kLaneMaxSlot; }
 
 // slot[i] of a batch whose bound exceeds the per-batch ceiling: no output
 // reserved (the scan counts 0), verdict DECOMP_OVERFLOW
@@ -209,7 +214,7 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
         // parts[pcap / 2..)); the rest to the wave decoders (zstd list at
         // wlist[0..), LZ list at wlist[n..))
         uint32_t sf = 0, sc = 0;
-        if (!over && sz > kLaneMaxSlot && decomp_wanted(descs[i], vres[i])) {
+        if (!over && sz > lane_max(vres[i].codec) && decomp_wanted(descs[i], vres[i])) {
             const uint32_t c = vres[i].codec;
             if (c == 2 || c == 3) {
                 const uint8_t* b = data + descs[i].offset + kHeaderSize;
@@ -326,7 +331,7 @@ __device__ __forceinline__ bool plan_slot(uint64_t& sz, uint64_t off, uint64_t o
     return true;
 }
 __device__ __forceinline__ bool wave_owned(const rpgpu_batch_desc& d, const rpgpu_batch_result& v, uint64_t sz) {
-    return decomp_wanted(d, v) && sz != kOverCeiling && sz > kLaneMaxSlot && (v.codec >= 2 && v.codec <= 4);
+    return decomp_wanted(d, v) && sz != kOverCeiling && sz > lane_max(v.codec) && (v.codec >= 2 && v.codec <= 4);
 }
 
 // LZ4 (CODEC 3, which also writes the verdict of every batch nobody decodes)
