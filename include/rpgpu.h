@@ -336,8 +336,9 @@ typedef struct rpgpu_decomp_result {
 } rpgpu_decomp_result;   /* 32 bytes */
 
 /* Scratch of the decompress path: the plan's slots and scans, the validation
- * scratch of the rewritten batches, and one ~19 KB zstd workspace per decoder
- * lane (min(n, 131072) lanes: up to 2.5 GB, sized for HBM, not for the host). */
+ * scratch of the rewritten batches, one ~20 KB zstd workspace per decoder
+ * lane (min(n, 131072) lanes: up to 2.6 GB, sized for HBM, not for the host)
+ * and the part list of split bodies (36 B per part, n + 4096 parts). */
 size_t rpgpu_decomp_scratch_bytes(uint32_t n);
 /* Plan: per-batch output slots and their exclusive scan into d_scratch;
  * *d_out_bytes = output bytes needed.  The output buffer must hold
