@@ -208,7 +208,7 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
         delete c;
         return nullptr;
     }
-    c->overlap.chunks = 4;
+    c->overlap.chunks = 16;  // C2 (1M batches): 4 / 8 / 16 / 32 chunks 4.74 / 4.71 / 4.63 / 4.83 ms, off 4.86
     if (const char* e = getenv("RPGPU_RUN_CHUNKS")) {
         const int v = atoi(e);
         if (v >= 1 && v <= rpgpu::kMaxRunChunks) c->overlap.chunks = v;
@@ -221,8 +221,10 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
     c->have_overlap = hipStreamCreateWithFlags(&c->overlap.aux, hipStreamNonBlocking) == hipSuccess;
     for (int k = 0; c->have_overlap && k <= c->overlap.chunks; k++)
         c->have_overlap = hipEventCreateWithFlags(&c->overlap.ev[k], hipEventDisableTiming) == hipSuccess;
-    // measured no faster at the default grid: opt-in
-    if (!getenv("RPGPU_OVERLAP")) c->have_overlap = false;
+    // on by default (RPGPU_OVERLAP=0 turns it off): the walk of chunk k runs
+    // beside the checksums of chunk k + 1
+    if (const char* e = getenv("RPGPU_OVERLAP"))
+        if (atoi(e) == 0) c->have_overlap = false;
     std::vector<uint32_t> t(rpgpu::kTableWords);
     rpgpu::build_tables(t.data());
     if (hipMalloc(&c->d_tables, sizeof(uint32_t) * t.size()) != hipSuccess ||
