@@ -176,7 +176,8 @@ def main() -> int:
         spec.payload = abi.PAYLOAD_TEXT if args.payload == "text" else abi.PAYLOAD_ALNUM
     if args.ops:
         spec.ops = args.ops
-    eng = engine.Engine(local)
+    # chunked checksum / walk overlap for the uniform uncompressed arenas (RPGPU_OPT_WALK_OVERLAP)
+    eng = engine.Engine(local, walk_overlap=not decompress)
     chunks, P_total, part_shift, (plo, phi) = rank_chunks(cfg, rank, world, scaling, args.batches)
     n = sum(m for _, m in chunks)
 

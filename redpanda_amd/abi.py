@@ -22,6 +22,7 @@ OP_HDRCRC = 2
 OP_PARSE = 4
 OP_INDEX = 8
 OP_DECOMP = 16
+OPT_WALK_OVERLAP = 1  # rpgpu_opts.flags: RPGPU_OPT_WALK_OVERLAP
 OP_RECRC = 32
 OPS_PRODUCE = OP_CRC | OP_HDRCRC | OP_PARSE | OP_INDEX
 

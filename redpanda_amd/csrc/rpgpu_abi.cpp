@@ -221,10 +221,11 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
     c->have_overlap = hipStreamCreateWithFlags(&c->overlap.aux, hipStreamNonBlocking) == hipSuccess;
     for (int k = 0; c->have_overlap && k <= c->overlap.chunks; k++)
         c->have_overlap = hipEventCreateWithFlags(&c->overlap.ev[k], hipEventDisableTiming) == hipSuccess;
-    // on by default (RPGPU_OVERLAP=0 turns it off): the walk of chunk k runs
-    // beside the checksums of chunk k + 1
-    if (const char* e = getenv("RPGPU_OVERLAP"))
-        if (atoi(e) == 0) c->have_overlap = false;
+    // the walk of chunk k beside the checksums of chunk k + 1:
+    // RPGPU_OPT_WALK_OVERLAP, or RPGPU_OVERLAP=1 / 0 to force it on / off
+    bool want_overlap = opts && (opts->flags & RPGPU_OPT_WALK_OVERLAP);
+    if (const char* e = getenv("RPGPU_OVERLAP")) want_overlap = atoi(e) != 0;
+    if (!want_overlap) c->have_overlap = false;
     std::vector<uint32_t> t(rpgpu::kTableWords);
     rpgpu::build_tables(t.data());
     if (hipMalloc(&c->d_tables, sizeof(uint32_t) * t.size()) != hipSuccess ||

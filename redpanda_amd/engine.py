@@ -30,9 +30,10 @@ def _stream(stream: int):
 class Engine:
     """One rpgpu context (one per Seastar shard x GPU in the reference's terms)."""
 
-    def __init__(self, device: int = 0, max_decoded_batch: int = 0):
+    def __init__(self, device: int = 0, max_decoded_batch: int = 0, walk_overlap: bool = False):
+        """walk_overlap: RPGPU_OPT_WALK_OVERLAP (arenas of many small, similar batches)."""
         self._lib = abi.lib()
-        opts = abi.Opts(0, 0, 0, max_decoded_batch)
+        opts = abi.Opts(abi.OPT_WALK_OVERLAP if walk_overlap else 0, 0, 0, max_decoded_batch)
         self._ctx = self._lib.rpgpu_open(device, C.byref(opts))
         if not self._ctx:
             raise EngineError(f"rpgpu_open({device}) failed (no usable HIP device?)")

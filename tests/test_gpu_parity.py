@@ -71,3 +71,19 @@ def test_crc32c_scalar_mirror(eng):
         b = rng.integers(0, 256, n, dtype=np.uint8)
         seed = int(rng.integers(0, 2**32))
         assert eng.crc32c_extend(seed, b) == orc.crc32c(b, seed), n
+
+
+@pytest.mark.parametrize("case", ["headers", "ragged"])
+def test_walk_overlap_arenas(case):
+    """RPGPU_OPT_WALK_OVERLAP: an arena above kRunChunkMin (16384 batches) is
+    checksummed in chunks with each chunk's walk on a second stream; results
+    and index as the oracle's (uniform small batches, and ragged ones whose
+    walks differ in length)."""
+    kw = dict(CASES[case])
+    if case == "ragged":
+        kw["body_max"] = 3000
+    spec = engine.make_spec(seed=zlib.crc32(case.encode()) + 7, format=abi.FMT_KAFKA_WIRE, **kw)
+    data, descs = engine.build_arena(spec, 20000)
+    with engine.Engine(0, walk_overlap=True) as e:
+        got = e.submit(data, descs)
+    assert_same(*got, *orc.validate_arena(data, descs))
