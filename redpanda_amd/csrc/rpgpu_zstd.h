@@ -85,7 +85,10 @@ constexpr uint32_t kHufMaxLog = 12;                   // HufLog: the DCtx's Huff
 // First-level Huffman table for workspaces in HBM: 256 entries (512 B, cache-resident
 // across a lane's symbols) that resolve every code of <= 8 bits; longer codes fall
 // through to the full table.  Same symbols and bit counts as the full table.
-constexpr uint32_t kHuf1Log = 8;
+#ifndef RPZ_HUF1_LOG
+#define RPZ_HUF1_LOG 8
+#endif
+constexpr uint32_t kHuf1Log = RPZ_HUF1_LOG;  // C4: 7 / 8 / 9 / 10 bits 551 / 558 / 572 / 594 ms
 constexpr uint16_t kHuf1None = 0xFFFF;
 
 // ------------------------------------------------------------------ tables
