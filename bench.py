@@ -107,6 +107,51 @@ def effective_cores() -> tuple[int, dict]:
     return max(1, t), {"affinity_cpus": aff, "cgroup_cpu_quota": quota, "machine_cpus": os.cpu_count()}
 
 
+def quiet_cpus(t: int, window: float = 0.3) -> list[int]:
+    """t CPUs of this job's affinity set on distinct physical cores, the least
+    busy over a short /proc/stat window first (the box is shared: CPUs another
+    job keeps busy would time that job, not the baseline)."""
+    aff = sorted(os.sched_getaffinity(0))
+
+    def ticks():
+        out = {}
+        try:
+            for line in open("/proc/stat"):
+                if line.startswith("cpu") and line[3].isdigit():
+                    f = line.split()
+                    v = list(map(int, f[1:]))
+                    out[int(f[0][3:])] = (sum(v) - v[3] - (v[4] if len(v) > 4 else 0), sum(v))
+        except OSError:
+            pass
+        return out
+
+    a = ticks()
+    time.sleep(window)
+    b = ticks()
+
+    def busy(c):
+        if c not in a or c not in b or b[c][1] == a[c][1]:
+            return 0.0
+        return (b[c][0] - a[c][0]) / (b[c][1] - a[c][1])
+
+    def core(c):
+        try:
+            return open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read().strip()
+        except OSError:
+            return str(c)
+
+    chosen, cores = [], set()
+    for c in sorted(aff, key=lambda c: (busy(c), c)):
+        k = core(c)
+        if k in cores:
+            continue
+        cores.add(k)
+        chosen.append(c)
+        if len(chosen) == t:
+            break
+    return sorted(chosen) if len(chosen) == t else aff[:t]
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -115,6 +160,59 @@ def cpu_model() -> str:
     except OSError:
         pass
     return "unknown"
+
+
+# ---- full parity check of a decompress run ---------------------------------------------------
+def full_check(spec, chunks, part_shift, res, dres, ores, index, gen_threads, piece=16384):
+    """Regenerates this rank's arena piece by piece (same seeds, so the same
+    bytes) and compares EVERY batch with the oracle: validation result,
+    decompress verdict and decoded length, the rewritten batch's validation
+    result (its crc / header_crc are CRCs of the decoded bytes) and its index
+    entries.  Returns mismatch counts and both verdict histograms."""
+    import oracle.oracle as orc
+    from redpanda_amd import abi, engine
+
+    T = max(1, min(16, len(os.sched_getaffinity(0))))
+    names = [f for f in abi.RESULT_DTYPE.names if f != "index_first"]
+    bad = np.zeros(len(res), dtype=bool)
+    kinds = {"validation": 0, "decomp_verdict": 0, "decoded_len": 0, "rewritten_result": 0, "index": 0}
+    hist_o = {}
+    at = 0
+    for first, m in chunks:
+        for k in range(0, m, piece):
+            c = min(piece, m - k)
+            sl = slice(at, at + c)
+            sdata, sdescs = engine.build_arena(spec, c, first=first + k, nthreads=gen_threads)
+            sdescs["partition"] += part_shift
+            oc = dres["out_cap"][sl].astype(np.int64)
+            caps = np.where(oc > 0, oc - 61 - 128, 0).astype(np.uint64)
+            r0, _, _ = orc.validate_arena(sdata, sdescs, nthreads=T, fast_crc=True)
+            w = orc.decompress_arena(sdata, sdescs, r0, caps, codecs=(1, 2, 3, 4), nthreads=T, fast_crc=True)
+            for kind, diff in (
+                    ("validation", np.any([res[f][sl] != r0[f] for f in names], axis=0)),
+                    ("decomp_verdict", dres["verdict"][sl] != w["verdicts"]),
+                    ("decoded_len", dres["out_len"][sl] != w["out_len"]),
+                    ("rewritten_result", np.any([ores[f][sl] != w["out_results"][f] for f in names], axis=0))):
+                kinds[kind] += int(diff.sum())
+                bad[sl] |= diff
+            # index entries: the rewritten batches' slices, in batch order on both sides
+            cnt = ores["index_count"][sl].astype(np.int64)
+            ofirst = w["out_results"]["index_first"].astype(np.int64)
+            for j in np.nonzero(cnt)[0]:
+                g0, o0, nn = int(ores["index_first"][at + j]), int(ofirst[j]), int(cnt[j])
+                if not np.array_equal(index[g0:g0 + nn], w["index"][o0:o0 + nn]):
+                    kinds["index"] += 1
+                    bad[at + j] = True
+            for v, n_ in zip(*np.unique(w["verdicts"], return_counts=True)):
+                name = abi.VERDICT_NAMES.get(int(v), str(int(v)))
+                hist_o[name] = hist_o.get(name, 0) + int(n_)
+            at += c
+    hist_g = {abi.VERDICT_NAMES.get(int(v), str(int(v))): int(n_)
+              for v, n_ in zip(*np.unique(dres["verdict"], return_counts=True))}
+    return {"batches": int(at), "mismatched_batches": int(bad.sum()), "mismatches_by_kind": kinds,
+            "decompress_verdicts_gpu": hist_g, "decompress_verdicts_oracle": hist_o,
+            "validation_verdicts_gpu": {abi.VERDICT_NAMES.get(int(v), str(int(v))): int(n_)
+                                        for v, n_ in zip(*np.unique(res["verdict"], return_counts=True))}}
 
 
 # ---- the workload of one rank ------------------------------------------------------------
@@ -148,6 +246,8 @@ def main() -> int:
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-runs", type=int, default=5)
     ap.add_argument("--ops", type=int, default=0, help="override the rpgpu_op mask (diagnostics)")
+    ap.add_argument("--full-check", type=int, default=-1,
+                    help="compare every batch of a decompress config with the oracle (default: on for c5)")
     ap.add_argument("--payload", default="text", choices=["text", "alnum"],
                     help="record payload of the compressed configs (text: Zipf words, alnum: random)")
     args = ap.parse_args()
@@ -395,6 +495,11 @@ def main() -> int:
             def cpu_pass(th):
                 return orc.validate_arena(sdata, sdescs, nthreads=th, fast_crc=True)
 
+        # one pinned worker thread per core of the job's CPU set (unpinned
+        # threads gave run-to-run spreads of 1.6x); min / median / max of the runs
+        pin = quiet_cpus(T)
+        orc.set_pin(pin)
+
         def timed(th):
             cpu_pass(th)  # warm-up
             ts = []
@@ -402,10 +507,11 @@ def main() -> int:
                 t1 = time.perf_counter()
                 cpu_pass(th)
                 ts.append(time.perf_counter() - t1)
-            return sw / float(np.median(ts)) / 1e9
+            g = sorted(sw / t / 1e9 for t in ts)
+            return float(np.median(g)), [round(g[0], 3), round(float(np.median(g)), 3), round(g[-1], 3)]
 
-        cpu1 = timed(1)
-        cpuT = timed(T) if T > 1 else cpu1
+        cpu1, spread1 = timed(1)
+        cpuT, spreadT = timed(T) if T > 1 else (cpu1, spread1)
         want = cpu_pass(T)
         # the GPU's timed output for the same batches must equal the oracle's
         names = [f for f in abi.RESULT_DTYPE.names if f != "index_first"]
@@ -433,16 +539,28 @@ def main() -> int:
             same = all(np.array_equal(res[f][:sample_n], ores_c[f]) for f in names)
             what = "record walk + index"
             checked = f"first {sample_n} batches"
+        orc.set_pin([])
         out["cpu_baseline"] = {
             "value": round(cpuT, 3), "unit": "GB/s", "cores": T, "kind": "port",
-            "single_thread_gbps": round(cpu1, 3), "cpu_model": cpu_model(), **hostinfo,
+            "single_thread_gbps": round(cpu1, 3), "min_median_max_gbps": spreadT,
+            "single_thread_min_median_max_gbps": spread1, "pinned_cpus": pin,
+            "cpu_model": cpu_model(), **hostinfo,
             "sample": f"first {sample_n} batches of this workload ({sw / 1e9:.3f} GB wire), median of "
                       f"{args.cpu_runs} runs after a warm-up, at 1 and {T} threads (partitions round-robin "
-                      f"over threads, one thread per Seastar shard): oracle/ C restatement (SSE4.2 "
+                      f"over threads, one thread per Seastar shard, each pinned to its own physical core: the least busy of the job's CPU set): oracle/ C restatement (SSE4.2 "
                       f"CRC32C) + {what}" + (" -- one partition, so one shard does all the work"
                                              if cfg["partitions"] == 1 else "")}
         out["gpu_matches_oracle_on_sample"] = bool(same)
         out["gpu_checked_batches"] = checked
+
+    full = args.full_check if args.full_check >= 0 else int(args.config == "c5")
+    if decompress and full:
+        # every batch's verdicts, decoded length, rewritten batch
+        # (its results: CRCs of the decoded bytes) and index against the oracle
+        out["full_check"] = full_check(spec, chunks, part_shift, res, dres, ores,
+                                       d_index2.cpu().numpy().view(abi.INDEX_DTYPE), gen_threads)
+        out["gpu_matches_oracle_on_all_batches"] = out["full_check"]["mismatched_batches"] == 0
+        log(f"[rank {rank}] full check: {out['full_check']}")
 
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -104,6 +104,9 @@ enum rpgpu_verdict {
                                       (storage/log_reader.cc:30-38)             */
     /* segment index (storage/index_state.cc:48-54) */
     RPGPU_V_INDEX_OFFSET_BELOW_BASE = 37, /* vassert: batch base offset below the segment's */
+    /* remote segment reader (cloud_storage/remote_segment.cc:808-815) */
+    RPGPU_V_REMOTE_DELTA_ASSERT = 38, /* vassert in rp_to_kafka: a batch's Redpanda
+                                      offset below the offset-translation delta */
     RPGPU_V_SKIPPED = 40,          /* not decompressed: no RPGPU_OP_DECOMP, not
                                       validated OK, or not compressed        */
 };
@@ -548,6 +551,67 @@ typedef struct rpgpu_segment_parse_result {
 int32_t rpgpu_segment_parse_device(rpgpu_ctx* ctx, const uint8_t* d_data, const rpgpu_segment_read* d_reads,
                                    uint32_t nreads, rpgpu_segment_parse_result* d_results,
                                    rpgpu_batch_desc* d_descs, void* hip_stream);
+
+/* ---- remote (tiered storage) segment reader ---------------------------------
+ * Replaces continuous_batch_parser::consume driving cloud_storage's
+ * remote_segment_batch_consumer (cloud_storage/remote_segment.cc:788-975): one
+ * remote_segment_batch_reader::read_some call (:1007-1050) per read.  The
+ * config's offsets are Kafka offsets, the segment's batches carry Redpanda
+ * offsets; rp_to_kafka(o) = o - cur_delta (:808-815).  Per batch:
+ * accept_batch_start (:846-900) stops past max_offset or over the byte budget,
+ * skips every batch that is not raft_data, and raft_data batches below
+ * start_offset or older than first_timestamp; skip_batch_start (:916-946)
+ * advances the config and, for raft_configuration / archival_metadata batches,
+ * records an offset-translation gap [base, last] and grows cur_delta by
+ * last_offset_delta + 1; consume_batch_end (:951-975) advances the config,
+ * produces the batch with its base offset rewritten to the Kafka offset and
+ * stops once the produced bytes pass max_consume_size (128 KiB, :61) or the
+ * budget is spent.  Produced batch k becomes an on-disk descriptor at
+ * d_descs[desc_first + k] with its Kafka base offset at
+ * d_kafka_base[desc_first + k] (k < desc_cap); gap g is d_gaps[2 * (gap_first
+ * + g)] = base, [.. + 1] = last (g < gap_cap).  Parser errors and statuses as
+ * rpgpu_segment_parse_device; an exception status is RPGPU_V_BAD_CODEC_THROW
+ * (the record_batch constructor of a codec 5..7 batch, model/record.h:582-585)
+ * or RPGPU_V_REMOTE_DELTA_ASSERT. */
+typedef struct rpgpu_remote_read {
+    uint64_t offset;          /* the stream's bytes in the arena              */
+    uint64_t length;          /* bytes the input stream yields                */
+    uint32_t desc_first, desc_cap;
+    uint32_t gap_first, gap_cap;
+    uint32_t partition;       /* copied into the emitted descriptors          */
+    uint8_t ops;              /* rpgpu_op mask of the emitted descriptors     */
+    uint8_t has_first_timestamp;
+    uint8_t strict_max_bytes;
+    uint8_t over_budget;      /* log_reader_config::over_budget on entry      */
+    int64_t start_offset;     /* log_reader_config (Kafka offsets)            */
+    int64_t max_offset;
+    int64_t first_timestamp;
+    int64_t cur_delta;        /* remote_segment_batch_reader::_cur_delta      */
+    int64_t cur_rp_offset;    /* remote_segment_batch_reader::_cur_rp_offset  */
+    uint64_t max_bytes, bytes_consumed;
+} rpgpu_remote_read;          /* 96 bytes */
+
+typedef struct rpgpu_remote_parse_result {
+    int32_t status;           /* as rpgpu_segment_parse_result.status (above) */
+    int32_t last_error;       /* the parser's _err                            */
+    uint32_t accepted;        /* batches produced (descriptors, up to cap)    */
+    uint32_t skipped;
+    uint64_t bytes_consumed;  /* the parser's _bytes_consumed                 */
+    int64_t start_offset;     /* log_reader_config::start_offset after (Kafka) */
+    uint64_t cfg_bytes_consumed;
+    int64_t cur_delta;        /* after the read                               */
+    int64_t cur_rp_offset;    /* after the read                               */
+    uint64_t produced_bytes;  /* remote_segment_batch_reader::_total_size     */
+    uint32_t gaps;            /* gaps recorded (all of them, even past gap_cap) */
+    uint8_t over_budget;
+    uint8_t stopped;          /* the consumer stopped the parser              */
+    uint16_t reserved;
+} rpgpu_remote_parse_result;  /* 72 bytes */
+
+int32_t rpgpu_remote_segment_parse_device(rpgpu_ctx* ctx, const uint8_t* d_data, const rpgpu_remote_read* d_reads,
+                                          uint32_t nreads, rpgpu_remote_parse_result* d_results,
+                                          rpgpu_batch_desc* d_descs, int64_t* d_kafka_base, int64_t* d_gaps,
+                                          void* hip_stream);
 
 /* ---- partition summaries (multi-GPU gather) -------------------------------
  * Per partition p of [part_lo, part_lo + nparts), over the batches of

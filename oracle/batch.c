@@ -413,6 +413,7 @@ struct arena_job {
 
 static void* arena_worker(void* arg) {
     struct arena_job* j = (struct arena_job*)arg;
+    orc_pin_thread(j->tid);
     for (uint32_t i = 0; i < j->n; i++) {
         const rpgpu_batch_desc* d = &j->descs[i];
         if ((int)(d->partition % (uint32_t)j->nthreads) != j->tid) continue;
@@ -445,12 +446,12 @@ uint64_t orc_validate_arena(const rpgpu_batch_desc* descs, uint32_t n,
     pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
     for (int t = 0; t < nthreads; t++) {
         jobs[t] = (struct arena_job){descs, n, data, res, idx, first, t, nthreads};
-        if (nthreads > 1)
+        if (nthreads > 1 || orc_pin_active())
             pthread_create(&th[t], NULL, arena_worker, &jobs[t]);
         else
             arena_worker(&jobs[t]);
     }
-    if (nthreads > 1)
+    if (nthreads > 1 || orc_pin_active())
         for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
     free(th);
     free(jobs);

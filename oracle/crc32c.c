@@ -13,10 +13,30 @@
  * Both are pinned by the RFC 3720 known answer crc32c("123456789")=0xE3069283
  * (tests/test_oracle.py).
  */
+#define _GNU_SOURCE
 #include "rporacle.h"
 
 #include <pthread.h>
+#include <sched.h>
 #include <string.h>
+
+/* ---- CPU-baseline thread pinning (bench.py): worker t runs on cpu[t % n] */
+static int g_pin[4096];
+static int g_npin;
+void orc_set_pin(const int* cpus, int n) {
+    if (n < 0) n = 0;
+    if (n > 4096) n = 4096;
+    for (int i = 0; i < n; i++) g_pin[i] = cpus[i];
+    g_npin = n;
+}
+int orc_pin_active(void) { return g_npin > 0; }
+void orc_pin_thread(int tid) {
+    if (!g_npin) return;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(g_pin[tid % g_npin], &set);
+    pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
 
 #define POLY 0x82F63B78u
 

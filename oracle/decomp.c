@@ -83,6 +83,7 @@ static void decompress_one(const struct dec_job* j, uint32_t i) {
 
 static void* dec_worker(void* arg) {
     const struct dec_job* j = (const struct dec_job*)arg;
+    orc_pin_thread(j->tid);
     for (uint32_t i = (uint32_t)j->tid; i < j->n; i += (uint32_t)j->nthreads) decompress_one(j, i);
     return NULL;
 }
@@ -97,12 +98,12 @@ void orc_decompress_batches(const rpgpu_batch_desc* descs, uint32_t n, const uin
     for (int t = 0; t < nthreads; t++) {
         jobs[t] = (struct dec_job){descs, n, data, vres, codec_mask, out, out_off, out_cap,
                                    verdicts, out_len, rdescs, t, nthreads};
-        if (nthreads > 1)
+        if (nthreads > 1 || orc_pin_active())
             pthread_create(&th[t], NULL, dec_worker, &jobs[t]);
         else
             dec_worker(&jobs[t]);
     }
-    if (nthreads > 1)
+    if (nthreads > 1 || orc_pin_active())
         for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
     free(th);
     free(jobs);

@@ -61,6 +61,8 @@ def lib() -> C.CDLL:
         L.orc_crc32c_extend_sse42.restype = u32
         L.orc_crc32c_extend_sse42.argtypes = [u32, vp, sz]
         L.orc_set_fast_crc.argtypes = [C.c_int]
+        L.orc_set_pin.argtypes = [vp, C.c_int]
+        L.orc_set_pin.restype = None
         L.orc_read_varlong.restype = C.c_int64
         L.orc_read_varlong.argtypes = [vp, sz, C.POINTER(sz), C.POINTER(u32)]
         L.orc_write_varlong.restype = sz
@@ -87,6 +89,8 @@ def lib() -> C.CDLL:
         L.orc_record_sets_reduce.restype = None
         L.orc_segment_parse.restype = None
         L.orc_segment_parse.argtypes = [vp, vp, vp, vp]
+        L.orc_remote_segment_parse.restype = None
+        L.orc_remote_segment_parse.argtypes = [vp, vp, vp, vp, vp, vp]
         L.orc_segment_index.restype = None
         L.orc_segment_index.argtypes = [vp, vp, vp, u32, vp, vp]
         L.orc_record_sets_reduce.argtypes = [u32, vp, vp, vp, vp, vp]
@@ -262,6 +266,25 @@ def segment_parse(data: np.ndarray, reads: np.ndarray):
     return res, descs[:ncap]
 
 
+def remote_segment_parse(data: np.ndarray, reads: np.ndarray):
+    """remote_segment_batch_reader::read_some per read (oracle/parse.c
+    orc_remote_segment_parse): (results, descs, kafka_base, gaps)."""
+    from redpanda_amd.abi import REMOTE_PARSE_RESULT_DTYPE, REMOTE_READ_DTYPE
+
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    reads = np.ascontiguousarray(reads, dtype=REMOTE_READ_DTYPE)
+    res = np.zeros(len(reads), dtype=REMOTE_PARSE_RESULT_DTYPE)
+    ncap = int((reads["desc_first"].astype(np.int64) + reads["desc_cap"]).max()) if len(reads) else 0
+    gcap = int((reads["gap_first"].astype(np.int64) + reads["gap_cap"]).max()) if len(reads) else 0
+    descs = np.zeros(max(ncap, 1), dtype=DESC_DTYPE)
+    kbase = np.zeros(max(ncap, 1), dtype=np.int64)
+    gaps = np.zeros((max(gcap, 1), 2), dtype=np.int64)
+    for i in range(len(reads)):
+        lib().orc_remote_segment_parse(data.ctypes.data, reads[i:i + 1].ctypes.data, res[i:i + 1].ctypes.data,
+                                       descs.ctypes.data, kbase.ctypes.data, gaps.ctypes.data)
+    return res, descs[:ncap], kbase[:ncap], gaps[:gcap]
+
+
 def compaction_keep(data: np.ndarray, descs: np.ndarray, results: np.ndarray, index: np.ndarray):
     """Which records survive self-compaction (oracle/compact.c): (keep, nkeys),
     keep[j] per index entry: 1 keep, 0 superseded, 2 not a record of an OK batch."""
@@ -337,3 +360,10 @@ def compress_batches(data: np.ndarray, descs: np.ndarray, results: np.ndarray, c
         h["header_crc"] = internal_header_only_crc(h)
         out.append(h.tobytes() + payload)
     return out
+
+
+def set_pin(cpus) -> None:
+    """Pin the arena drivers' worker thread t to cpus[t % len(cpus)] (CPU
+    baseline timing); an empty list unpins."""
+    arr = np.ascontiguousarray(list(cpus), dtype=np.int32)
+    lib().orc_set_pin(arr.ctypes.data if len(arr) else None, len(arr))

@@ -38,7 +38,7 @@ void orc_segment_parse(const uint8_t* data, const rpgpu_segment_read* rd, rpgpu_
     const uint64_t max_buffer = rd->max_buffer ? rd->max_buffer : 32 * 1024;
     uint64_t pos = 0, bytes_consumed = 0, phys = 0, buffer = 0;
     int32_t err = RPGPU_V_OK;
-    int exception = 0, stopped = 0;
+    int exception = 0, stopped = 0, codec_throw = 0;
     uint32_t accepted = 0, skipped = 0;
     /* reader + consumer state */
     int64_t start_offset = rd->start_offset, expected = rd->expected_next_batch;
@@ -129,6 +129,13 @@ void orc_segment_parse(const uint8_t* data, const rpgpu_segment_read* rd, rpgpu_
             break;
         }
         pos += HDR + body;
+        if (reader && (h.attrs & 7) > 4) {
+            /* consume_batch_end constructs record_batch(tag_ctor_ng), whose
+             * attrs.compression() throws for codec 5..7 (model/record.h:283-300,
+             * 582-585): the exception escapes consume() */
+            codec_throw = 1;
+            break;
+        }
         if (reader) { /* consume_batch_end (:92-121) with add_one (:152-163) */
             start_offset = last + 1;
             cfg_bytes += (uint64_t)(int64_t)h.size_bytes;
@@ -145,9 +152,11 @@ void orc_segment_parse(const uint8_t* data, const rpgpu_segment_read* rd, rpgpu_
          * header read ends the loop with end_of_stream */
     }
     memset(out, 0, sizeof(*out));
-    out->last_error = exception ? RPGPU_V_OK : err;
+    out->last_error = (exception || codec_throw) ? RPGPU_V_OK : err;
     if (exception)
         out->status = RPGPU_V_READ_OFFSET_REGRESSION;
+    else if (codec_throw)
+        out->status = RPGPU_V_BAD_CODEC_THROW;
     else if (bytes_consumed || benign(err))
         out->status = RPGPU_V_OK; /* :283-296 partial reads are results */
     else
@@ -159,6 +168,163 @@ void orc_segment_parse(const uint8_t* data, const rpgpu_segment_read* rd, rpgpu_
     out->start_offset = start_offset;
     out->cfg_bytes_consumed = cfg_bytes;
     out->expected_next_batch = expected;
+    out->over_budget = (uint8_t)over_budget;
+    out->stopped = (uint8_t)stopped;
+}
+
+
+/*
+ * cloud_storage::remote_segment_batch_consumer (cloud_storage/remote_segment.cc:
+ * 788-975) under continuous_batch_parser::consume, i.e. one read_some call of
+ * remote_segment_batch_reader (:1007-1050).  Offsets in the config are Kafka
+ * offsets; the batches carry Redpanda offsets, translated with the reader's
+ * running delta (_cur_delta).  Only raft_data batches are produced; skipped
+ * raft_configuration / archival_metadata batches are offset-translation gaps
+ * that grow the delta (skip_batch_start :916-946).  consume_batch_end
+ * (:951-975) rewrites the produced batch's base offset to its Kafka offset
+ * and stops once the produced bytes pass max_consume_size (128 KiB, :61).
+ */
+#define MAX_CONSUME_SIZE (128u * 1024u)
+#define TYPE_RAFT_DATA 1
+#define TYPE_RAFT_CONFIGURATION 2
+#define TYPE_ARCHIVAL_METADATA 19
+
+void orc_remote_segment_parse(const uint8_t* data, const rpgpu_remote_read* rd, rpgpu_remote_parse_result* out,
+                              rpgpu_batch_desc* descs, int64_t* kafka_base, int64_t* gaps) {
+    const uint8_t* seg = data + rd->offset;
+    const uint64_t len = rd->length;
+    uint64_t pos = 0, bytes_consumed = 0, produced = 0;
+    int32_t err = RPGPU_V_OK, thrown = RPGPU_V_OK;
+    int stopped = 0, over_budget = rd->over_budget;
+    uint32_t accepted = 0, skipped = 0, ngaps = 0;
+    int64_t start_offset = rd->start_offset, delta = rd->cur_delta, cur_rp = rd->cur_rp_offset;
+    uint64_t cfg_bytes = rd->bytes_consumed;
+    for (;;) {
+        uint64_t rem = len - pos;
+        if (rem == 0) {
+            err = RPGPU_V_END_OF_STREAM;
+            break;
+        }
+        if (rem < HDR) {
+            err = RPGPU_V_STREAM_SHORT;
+            break;
+        }
+        const uint8_t* p = seg + pos;
+        if (all_zero(p, HDR)) {
+            err = RPGPU_V_FALLOCATED_ZERO;
+            break;
+        }
+        rpgpu_rp_header h;
+        memcpy(&h, p, sizeof(h));
+        if (orc_internal_header_only_crc(&h) != h.header_crc) {
+            err = RPGPU_V_HDR_CRC_MISMATCH;
+            break;
+        }
+        const int64_t last = h.base_offset + h.last_offset_delta;
+        /* accept_batch_start (:846-900); rp_to_kafka vasserts k >= delta (:808-815) */
+        int decision = ACCEPT;
+        if (h.base_offset < delta) {
+            thrown = RPGPU_V_REMOTE_DELTA_ASSERT;
+            break;
+        }
+        if (h.base_offset - delta > rd->max_offset) {
+            decision = STOP;
+        } else if (h.type != TYPE_RAFT_DATA) {
+            decision = SKIP;
+        } else if (last < delta) {
+            thrown = RPGPU_V_REMOTE_DELTA_ASSERT;
+            break;
+        } else if (last - delta < start_offset) {
+            decision = SKIP;
+        } else if ((rd->strict_max_bytes || cfg_bytes) && cfg_bytes + (uint64_t)(int64_t)h.size_bytes > rd->max_bytes) {
+            over_budget = 1;
+            decision = STOP;
+        } else if (rd->has_first_timestamp && rd->first_timestamp > h.max_timestamp) {
+            decision = SKIP;
+        }
+        if (decision == STOP) {
+            stopped = 1;
+            break;
+        }
+        const uint64_t body = (uint64_t)((int64_t)h.size_bytes - HDR);
+        const uint64_t avail = len - pos - HDR;
+        if (decision == SKIP) {
+            /* skip_batch_start (:916-946): advance_config_offsets, then the gap */
+            cur_rp = last + 1;
+            if (h.type == TYPE_RAFT_DATA) { /* rp_to_kafka(last) checked above */
+                const int64_t next = last - delta + 1;
+                if (next > start_offset) start_offset = next;
+            }
+            if (h.type == TYPE_RAFT_CONFIGURATION || h.type == TYPE_ARCHIVAL_METADATA) {
+                if (ngaps < rd->gap_cap) {
+                    gaps[2 * ((size_t)rd->gap_first + ngaps)] = h.base_offset;
+                    gaps[2 * ((size_t)rd->gap_first + ngaps) + 1] = last;
+                }
+                ngaps++;
+                delta += (int64_t)h.last_offset_delta + 1;
+            }
+            if (body > avail) {
+                err = RPGPU_V_STREAM_SHORT;
+                break;
+            }
+            pos += HDR + body;
+            bytes_consumed += (uint64_t)(int64_t)h.size_bytes;
+            skipped++;
+            continue;
+        }
+        /* accept: consume_batch_start, consume_records */
+        bytes_consumed += (uint64_t)(int64_t)h.size_bytes;
+        if (body > avail) {
+            err = RPGPU_V_STREAM_SHORT;
+            break;
+        }
+        pos += HDR + body;
+        /* consume_batch_end (:951-975) */
+        if ((h.attrs & 7) > 4) { /* record_batch(tag_ctor_ng) throws: model/record.h:582-585 */
+            thrown = RPGPU_V_BAD_CODEC_THROW;
+            break;
+        }
+        cfg_bytes += (uint64_t)(int64_t)h.size_bytes;
+        cur_rp = last + 1;
+        {
+            const int64_t next = last - delta + 1;
+            if (next > start_offset) start_offset = next;
+        }
+        if (accepted < rd->desc_cap) {
+            rpgpu_batch_desc* d = &descs[rd->desc_first + accepted];
+            d->offset = rd->offset + pos - HDR - body;
+            d->length = (uint32_t)(body + HDR);
+            d->partition = rd->partition;
+            d->format = RPGPU_FMT_RP_DISK;
+            d->ops = rd->ops;
+            d->flags = 0;
+            d->reserved = 0;
+            kafka_base[rd->desc_first + accepted] = h.base_offset - delta;
+        }
+        accepted++;
+        produced += (uint64_t)(int64_t)h.size_bytes; /* remote_segment_batch_reader::produce (:1073-1079) */
+        if (over_budget || produced > MAX_CONSUME_SIZE) {
+            stopped = 1;
+            break;
+        }
+    }
+    memset(out, 0, sizeof(*out));
+    out->last_error = thrown != RPGPU_V_OK ? RPGPU_V_OK : err;
+    if (thrown != RPGPU_V_OK)
+        out->status = thrown;
+    else if (bytes_consumed || benign(err))
+        out->status = RPGPU_V_OK;
+    else
+        out->status = err;
+    out->accepted = accepted < rd->desc_cap ? accepted : rd->desc_cap;
+    out->skipped = skipped;
+    out->bytes_consumed = bytes_consumed;
+    out->start_offset = start_offset;
+    out->cfg_bytes_consumed = cfg_bytes;
+    out->cur_delta = delta;
+    out->cur_rp_offset = cur_rp;
+    out->produced_bytes = produced;
+    out->gaps = ngaps;
     out->over_budget = (uint8_t)over_budget;
     out->stopped = (uint8_t)stopped;
 }

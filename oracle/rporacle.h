@@ -29,6 +29,12 @@ uint32_t orc_crc32c_extend_sse42(uint32_t crc, const uint8_t* p, size_t n);
 int orc_have_sse42(void);
 /* select the body CRC used by the batch functions (0 = table, 1 = SSE4.2) */
 void orc_set_fast_crc(int fast);
+/* CPU-baseline thread pinning: worker thread t of the arena drivers runs on
+ * cpus[t % n] (n = 0: unpinned).  A pinned single-thread run uses a worker
+ * thread too, so the caller's own affinity never changes. */
+void orc_set_pin(const int* cpus, int n);
+int orc_pin_active(void);
+void orc_pin_thread(int tid);
 
 /* utils/vint.h:35-64,154-161 via bytes/iobuf_parser.h:48-52 */
 int64_t orc_read_varlong(const uint8_t* p, size_t n, size_t* pos, uint32_t* nbytes);
@@ -111,6 +117,10 @@ void orc_segment_index(const rpgpu_batch_desc* descs, const rpgpu_batch_result* 
  * the checksumming / skipping consumers (oracle/parse.c) */
 void orc_segment_parse(const uint8_t* data, const rpgpu_segment_read* rd, rpgpu_segment_parse_result* out,
                        rpgpu_batch_desc* descs);
+/* the same parser driving cloud_storage's remote_segment_batch_consumer
+ * (cloud_storage/remote_segment.cc:788-975, oracle/parse.c) */
+void orc_remote_segment_parse(const uint8_t* data, const rpgpu_remote_read* rd, rpgpu_remote_parse_result* out,
+                              rpgpu_batch_desc* descs, int64_t* kafka_base, int64_t* gaps);
 
 /* Compaction keys and batch timequery (compact.c): rpgpu_compaction_keep_device
  * and rpgpu_batch_timequery_device, restated sequentially. */

@@ -49,6 +49,7 @@ V_DECOMP_UNSUPPORTED = 33
 V_DECOMP_OVERFLOW = 34
 V_SET_HEADER_SHORT = 36
 V_INDEX_OFFSET_BELOW_BASE = 37
+V_REMOTE_DELTA_ASSERT = 38
 V_SKIPPED = 40
 
 VERDICT_NAMES = {v: k for k, v in globals().items() if k.startswith("V_") and isinstance(v, int)}
@@ -114,6 +115,18 @@ SEGMENT_PARSE_RESULT_DTYPE = np.dtype([("status", "<i4"), ("last_error", "<i4"),
                                        ("expected_next_batch", "<i8"), ("over_budget", "u1"), ("stopped", "u1"),
                                        ("reserved0", "<u2"), ("reserved1", "<u4")])
 assert SEGMENT_READ_DTYPE.itemsize == 112 and SEGMENT_PARSE_RESULT_DTYPE.itemsize == 64
+REMOTE_READ_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u8"), ("desc_first", "<u4"), ("desc_cap", "<u4"),
+                              ("gap_first", "<u4"), ("gap_cap", "<u4"), ("partition", "<u4"), ("ops", "u1"),
+                              ("has_first_timestamp", "u1"), ("strict_max_bytes", "u1"), ("over_budget", "u1"),
+                              ("start_offset", "<i8"), ("max_offset", "<i8"), ("first_timestamp", "<i8"),
+                              ("cur_delta", "<i8"), ("cur_rp_offset", "<i8"), ("max_bytes", "<u8"),
+                              ("bytes_consumed", "<u8")])
+REMOTE_PARSE_RESULT_DTYPE = np.dtype([("status", "<i4"), ("last_error", "<i4"), ("accepted", "<u4"),
+                                      ("skipped", "<u4"), ("bytes_consumed", "<u8"), ("start_offset", "<i8"),
+                                      ("cfg_bytes_consumed", "<u8"), ("cur_delta", "<i8"), ("cur_rp_offset", "<i8"),
+                                      ("produced_bytes", "<u8"), ("gaps", "<u4"), ("over_budget", "u1"),
+                                      ("stopped", "u1"), ("reserved", "<u2")])
+assert REMOTE_READ_DTYPE.itemsize == 96 and REMOTE_PARSE_RESULT_DTYPE.itemsize == 72
 TIMEQUERY_DTYPE = np.dtype([("batch", "<u4"), ("reserved", "<u4"), ("time", "<i8")])
 TIMEQUERY_RESULT_DTYPE = np.dtype([("offset", "<i8"), ("time", "<i8"), ("status", "<i4"), ("reserved", "<u4")])
 assert TIMEQUERY_DTYPE.itemsize == 16 and TIMEQUERY_RESULT_DTYPE.itemsize == 24
@@ -213,6 +226,7 @@ def lib() -> C.CDLL:
         _sig(L.rpgpu_kafka_error_code, _i32, _vp, _u32)
         _sig(L.rpgpu_kafka_error_codes_device, _i32, _vp, _vp, _u32, _u32, _vp, _vp)
         _sig(L.rpgpu_segment_parse_device, _i32, _vp, _vp, _vp, _u32, _vp, _vp, _vp)
+        _sig(L.rpgpu_remote_segment_parse_device, _i32, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp)
         _sig(L.rpgpu_partition_summaries_device, _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
         _sig(L.rpgpu_compaction_scratch_bytes, C.c_size_t, _u64)
         _sig(L.rpgpu_compaction_keep_device, _i32, _vp, _vp, _vp, _vp, _u32, _vp, _u64, _vp, _vp, _vp, _vp)
@@ -258,7 +272,7 @@ EXPORTED = [
     "rpgpu_abi_version", "rpgpu_open", "rpgpu_close", "rpgpu_last_error", "rpgpu_device_info",
     "rpgpu_arena_alloc", "rpgpu_arena_free", "rpgpu_submit", "rpgpu_poll", "rpgpu_wait",
     "rpgpu_eventfd", "rpgpu_kafka_error_code", "rpgpu_kafka_error_codes_device",
-    "rpgpu_partition_summaries_device", "rpgpu_segment_parse_device",
+    "rpgpu_partition_summaries_device", "rpgpu_segment_parse_device", "rpgpu_remote_segment_parse_device",
     "rpgpu_compaction_scratch_bytes", "rpgpu_compaction_keep_device", "rpgpu_batch_timequery_device",
     "rpgpu_kafka_serialize_device", "rpgpu_compress_scratch_bytes", "rpgpu_compress_plan_device",
     "rpgpu_compress_run_device",

@@ -67,8 +67,13 @@ hipError_t launch_kafka_codes(const rpgpu_batch_result* d_res, uint32_t n, uint3
 hipError_t launch_segment_parse(const uint8_t* d_data, const rpgpu_segment_read* d_reads, uint32_t n,
                                 rpgpu_segment_parse_result* d_res, rpgpu_batch_desc* d_descs,
                                 const uint32_t* d_tables, int grid, hipStream_t s);
+hipError_t launch_remote_parse(const uint8_t* d_data, const rpgpu_remote_read* d_reads, uint32_t n,
+                               rpgpu_remote_parse_result* d_res, rpgpu_batch_desc* d_descs, int64_t* d_kafka_base,
+                               int64_t* d_gaps, const uint32_t* d_tables, int grid, hipStream_t s);
 hipError_t launch_summaries(const rpgpu_batch_desc* d_descs, const rpgpu_batch_result* d_res, uint32_t n,
-                            uint32_t part_lo, uint32_t nparts, int64_t* d_out, hipStream_t s);
+                            uint32_t part_lo, uint32_t nparts, int64_t* d_out, hipStream_t s, int64_t* d_partial,
+                            int cu_count);
+size_t summary_scratch_bytes(int cu_count);
 size_t compaction_scratch_bytes(uint64_t index_cap);
 hipError_t launch_compaction_keep(const uint8_t* d_data, const rpgpu_batch_desc* d_descs,
                                   const rpgpu_batch_result* d_res, uint32_t n, const rpgpu_record_index* d_index,
@@ -135,6 +140,7 @@ struct rpgpu_ctx {
     rpgpu::DecompStreams dstreams{};  // large-batch wave decoders beside the lane decoders
     bool have_dstreams = false;
     uint32_t* d_tables = nullptr;
+    int64_t* d_sum_partial = nullptr;  // partition summaries: per-workgroup tables
     DevBuf work;     // submissions: descs | data | results | index | scratch | used
     DevBuf small;    // scalar mirrors
     DevBuf small_out;  // scalar mirrors: decompression output
@@ -234,6 +240,9 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
         rpgpu_close(c);
         return nullptr;
     }
+    // not fatal: without it the summaries take the global-atomic path
+    if (hipMalloc(&c->d_sum_partial, rpgpu::summary_scratch_bytes(c->cu_count)) != hipSuccess)
+        c->d_sum_partial = nullptr;
     return c;
 }
 
@@ -250,6 +259,7 @@ void rpgpu_close(rpgpu_ctx* c) {
     c->small.release();
     c->small_out.release();
     if (c->d_tables) (void)hipFree(c->d_tables);
+    if (c->d_sum_partial) (void)hipFree(c->d_sum_partial);
     if (c->overlap.aux) {
         (void)hipStreamSynchronize(c->overlap.aux);
         (void)hipStreamDestroy(c->overlap.aux);
@@ -285,12 +295,26 @@ int32_t rpgpu_segment_parse_device(rpgpu_ctx* c, const uint8_t* d_data, const rp
     return RPGPU_OK;
 }
 
+int32_t rpgpu_remote_segment_parse_device(rpgpu_ctx* c, const uint8_t* d_data, const rpgpu_remote_read* d_reads,
+                                          uint32_t nreads, rpgpu_remote_parse_result* d_results,
+                                          rpgpu_batch_desc* d_descs, int64_t* d_kafka_base, int64_t* d_gaps,
+                                          void* hip_stream) {
+    if (!c || (nreads && (!d_data || !d_reads || !d_results || !d_descs || !d_kafka_base || !d_gaps)))
+        return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_remote_parse(d_data, d_reads, nreads, d_results, d_descs, d_kafka_base, d_gaps,
+                                              c->d_tables, c->grid, s);
+    if (e != hipSuccess) return fail(c, e, "remote segment parse launch");
+    return RPGPU_OK;
+}
+
 int32_t rpgpu_partition_summaries_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs,
                                          const rpgpu_batch_result* d_results, uint32_t n, uint32_t part_lo,
                                          uint32_t nparts, int64_t* d_out, void* hip_stream) {
     if (!c || (n && (!d_descs || !d_results)) || (nparts && !d_out)) return RPGPU_EINVAL;
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
-    hipError_t e = rpgpu::launch_summaries(d_descs, d_results, n, part_lo, nparts, d_out, s);
+    hipError_t e = rpgpu::launch_summaries(d_descs, d_results, n, part_lo, nparts, d_out, s, c->d_sum_partial,
+                                           c->cu_count);
     if (e != hipSuccess) return fail(c, e, "summaries launch");
     return RPGPU_OK;
 }

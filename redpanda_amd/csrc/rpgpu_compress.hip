@@ -158,8 +158,12 @@ __global__ __launch_bounds__(256) void compress_lane_kernel(
         uint64_t len = 0;
         uint8_t ops = 0;
         if (comp_wanted(v)) {
-            if (off + sz > out_cap) {
-                verdict = RPGPU_V_DECOMP_OVERFLOW;  // caller's buffer smaller than the plan
+            const uint64_t need = kHeaderSize + comp_bound(CODEC, (uint64_t)(uint32_t)v.size_bytes - kHeaderSize) +
+                                  kCompSlack;
+            if (off + sz > out_cap || sz < need) {
+                // caller's buffer smaller than the plan, or a slot planned for a
+                // codec with a smaller bound than this run's
+                verdict = RPGPU_V_DECOMP_OVERFLOW;
             } else {
                 const uint8_t* p = data + d.offset;
                 uint8_t* o = out + off;

@@ -224,8 +224,20 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
                 const uint32_t np = c == 3 ? rpcodec::lz4f_split(b, body, half, none)
                                            : rpcodec::snappy_java_split(b, body, half, none);
                 if (np) {
-                    const uint32_t k0 = atomicAdd(wcount + (c == 3 ? 2 : 3), np);
-                    if (k0 + np <= half) {
+                    // reserve np part slots only if they fit: a reservation that
+                    // overflowed would leave slots nobody writes
+                    uint32_t* const pc = wcount + (c == 3 ? 2 : 3);
+                    uint32_t k0 = __hip_atomic_load(pc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    bool fit = false;
+                    while (k0 + np <= half) {
+                        const uint32_t prev = atomicCAS(pc, k0, k0 + np);
+                        if (prev == k0) {
+                            fit = true;
+                            break;
+                        }
+                        k0 = prev;
+                    }
+                    if (fit) {
                         SplitPart* const pp = parts + (c == 3 ? 0 : half) + k0;
                         auto put = [&](uint32_t k, uint32_t kind, uint64_t io, uint64_t il, uint64_t oo, uint64_t oc,
                                        uint32_t h) {
@@ -584,6 +596,21 @@ __global__ __launch_bounds__(64) void uncompress_one_kernel(uint32_t codec, cons
     }
 }
 
+// Queue counters (scratch `counter`): 0 / 1 LZ / zstd wave queue heads, 2 / 3
+// zstd / LZ wave list lengths, 4 / 5 LZ4 / snappy parts, 6 the plan's LZ list
+// length.  A run appends split fallbacks to the LZ list, so each run starts
+// from the plan's length (a plan may be run any number of times).
+__global__ void decomp_counters_kernel(uint32_t* c, uint32_t run) {
+    if (threadIdx.x != 0) return;
+    if (run) {
+        c[0] = 0;
+        c[1] = 0;
+        c[3] = c[6];
+    } else {
+        c[6] = c[3];
+    }
+}
+
 // ------------------------------------------------------------ launchers
 hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                               const rpgpu_batch_result* d_vres, uint64_t* d_out_bytes, void* d_scratch,
@@ -603,6 +630,8 @@ hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const
                                                  part_cap(n));
     e = hipGetLastError();
     if (e != hipSuccess) return e;
+    decomp_counters_kernel<<<1, 64, 0, s>>>(p.counter, 0);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     return launch_block_scan(p.block_sum, nb, d_out_bytes, s);
 }
 
@@ -615,7 +644,8 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     if (n == 0) return d_index_used ? hipMemsetAsync(d_index_used, 0, sizeof(uint64_t), s) : hipSuccess;
     const Parts p = parts(d_scratch, n);
     const uint32_t nblk = (n + 255) / 256;
-    hipError_t e = hipMemsetAsync(p.counter, 0, 2 * sizeof(uint32_t), s);
+    decomp_counters_kernel<<<1, 64, 0, s>>>(p.counter, 1);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // large batches on the wave decoders, on a second stream beside the lanes
     hipStream_t ws = s;

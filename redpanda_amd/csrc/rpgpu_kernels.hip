@@ -730,6 +730,7 @@ __global__ __launch_bounds__(kValidateThreads) void segment_parse_kernel(
         uint64_t pos = 0, bytes_consumed = 0, phys = 0, buffer = 0;
         int32_t err = RPGPU_V_OK;
         bool exception = false, stopped = false, over_budget = false;
+        bool codec_throw = false;
         uint32_t accepted = 0, skipped = 0;
         int64_t start_offset = rd.start_offset, expected = rd.expected_next_batch;
         uint64_t cfg_bytes = rd.bytes_consumed;
@@ -828,6 +829,12 @@ __global__ __launch_bounds__(kValidateThreads) void segment_parse_kernel(
                 break;
             }
             pos += kHeaderSize + body;
+            if (reader && (H.byte(21) & 7u) > 4u) {
+                // consume_batch_end's record_batch(tag_ctor_ng) throws for codec
+                // 5..7 (model/record.h:283-300,582-585)
+                codec_throw = true;
+                break;
+            }
             if (reader) {
                 start_offset = last + 1;
                 cfg_bytes += sz;
@@ -842,9 +849,11 @@ __global__ __launch_bounds__(kValidateThreads) void segment_parse_kernel(
         }
         if (l == 0) {
             rpgpu_segment_parse_result r;
-            r.last_error = exception ? RPGPU_V_OK : err;
+            r.last_error = (exception || codec_throw) ? RPGPU_V_OK : err;
             const bool benign = err == RPGPU_V_OK || err == RPGPU_V_END_OF_STREAM || err == RPGPU_V_FALLOCATED_ZERO;
-            r.status = exception ? RPGPU_V_READ_OFFSET_REGRESSION : ((bytes_consumed || benign) ? RPGPU_V_OK : err);
+            r.status = exception     ? RPGPU_V_READ_OFFSET_REGRESSION
+                       : codec_throw ? RPGPU_V_BAD_CODEC_THROW
+                                     : ((bytes_consumed || benign) ? RPGPU_V_OK : err);
             r.accepted = accepted < rd.desc_cap ? accepted : rd.desc_cap;
             r.skipped = skipped;
             r.bytes_consumed = bytes_consumed;
@@ -859,6 +868,185 @@ __global__ __launch_bounds__(kValidateThreads) void segment_parse_kernel(
             results[s] = r;
         }
     }
+}
+
+// ---------------------------------------- remote (tiered storage) segment reader
+// continuous_batch_parser::consume driving cloud_storage's
+// remote_segment_batch_consumer (cloud_storage/remote_segment.cc:788-975), one
+// wavefront per read (one read_some call), same header step as
+// segment_parse_kernel; the consumer's decisions are wave-uniform.
+constexpr uint64_t kMaxConsumeSize = 128u * 1024u;  // remote_segment.cc:61
+constexpr int8_t kTypeRaftData = 1, kTypeRaftConfiguration = 2, kTypeArchivalMetadata = 19;
+
+__global__ __launch_bounds__(kValidateThreads) void remote_parse_kernel(
+    const uint8_t* __restrict__ data, const rpgpu_remote_read* __restrict__ reads, uint32_t nreads,
+    rpgpu_remote_parse_result* __restrict__ results, rpgpu_batch_desc* __restrict__ descs,
+    int64_t* __restrict__ kafka_base, int64_t* __restrict__ gaps, const uint32_t* __restrict__ tables) {
+    __shared__ __attribute__((aligned(16))) uint32_t sT[kTableWords];
+    load_tables(sT, tables);
+    const uint32_t l = lane_id();
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    for (uint32_t s = gw; s < nreads; s += nw) {
+        const rpgpu_remote_read rd = reads[s];
+        const uint8_t* seg = data + rd.offset;
+        const uint64_t len = rd.length;
+        uint64_t pos = 0, bytes_consumed = 0, produced = 0;
+        int32_t err = RPGPU_V_OK, thrown = RPGPU_V_OK;
+        bool stopped = false, over_budget = rd.over_budget != 0;
+        uint32_t accepted = 0, skipped = 0, ngaps = 0;
+        int64_t start_offset = rd.start_offset, delta = rd.cur_delta, cur_rp = rd.cur_rp_offset;
+        uint64_t cfg_bytes = rd.bytes_consumed;
+        const __amdgpu_buffer_rsrc_t rs = batch_rsrc(seg);
+        for (;;) {
+            const uint64_t rem = len - pos;
+            if (rem == 0) {
+                err = RPGPU_V_END_OF_STREAM;
+                break;
+            }
+            if (rem < (uint64_t)kHeaderSize) {
+                err = RPGPU_V_STREAM_SHORT;
+                break;
+            }
+            const uint32_t hv = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int32_t)(pos + 4 * (l & 15)), 0, 0);
+            Img64 H;
+#pragma unroll
+            for (int i = 0; i < 16; i++) H.w[i] = rdl(hv, i);
+            if (header_all_zero(H)) {
+                err = RPGPU_V_FALLOCATED_ZERO;
+                break;
+            }
+            Img64 D;
+#pragma unroll
+            for (int i = 0; i < 16; i++) D.w[i] = H.w[i];
+            D.w[15] &= 0xffu;
+            if (header_crc_vec(sT, D) != H.w[0]) {
+                err = RPGPU_V_HDR_CRC_MISMATCH;
+                break;
+            }
+            const int32_t size_bytes = (int32_t)H.get_le(4, 4);
+            const int64_t base_offset = (int64_t)H.get_le(8, 8);
+            const int8_t type = (int8_t)H.byte(16);
+            const uint32_t codec = H.byte(21) & 7u;
+            const int32_t lod = (int32_t)H.get_le(23, 4);
+            const int64_t max_ts = (int64_t)H.get_le(35, 8);
+            const int64_t last = base_offset + lod;
+            const uint64_t sz = (uint64_t)(int64_t)size_bytes;
+            // accept_batch_start (remote_segment.cc:846-900); rp_to_kafka
+            // vasserts its argument is not below the delta (:808-815)
+            int decision = 0;  // 0 accept, 1 skip, 2 stop
+            if (base_offset < delta) {
+                thrown = RPGPU_V_REMOTE_DELTA_ASSERT;
+                break;
+            }
+            if (base_offset - delta > rd.max_offset) {
+                decision = 2;
+            } else if (type != kTypeRaftData) {
+                decision = 1;
+            } else if (last < delta) {
+                thrown = RPGPU_V_REMOTE_DELTA_ASSERT;
+                break;
+            } else if (last - delta < start_offset) {
+                decision = 1;
+            } else if ((rd.strict_max_bytes || cfg_bytes) && cfg_bytes + sz > rd.max_bytes) {
+                over_budget = true;
+                decision = 2;
+            } else if (rd.has_first_timestamp && rd.first_timestamp > max_ts) {
+                decision = 1;
+            }
+            if (decision == 2) {
+                stopped = true;
+                break;
+            }
+            const uint64_t body = (uint64_t)((int64_t)size_bytes - kHeaderSize);
+            const uint64_t avail = len - pos - kHeaderSize;
+            if (decision == 1) {
+                // skip_batch_start (:916-946): advance_config_offsets, then the
+                // offset-translation gap of a configuration / archival batch
+                cur_rp = last + 1;
+                if (type == kTypeRaftData && last - delta + 1 > start_offset) start_offset = last - delta + 1;
+                if (type == kTypeRaftConfiguration || type == kTypeArchivalMetadata) {
+                    if (ngaps < rd.gap_cap && l == 0) {
+                        gaps[2 * ((uint64_t)rd.gap_first + ngaps)] = base_offset;
+                        gaps[2 * ((uint64_t)rd.gap_first + ngaps) + 1] = last;
+                    }
+                    ngaps++;
+                    delta += (int64_t)lod + 1;
+                }
+                if (body > avail) {
+                    err = RPGPU_V_STREAM_SHORT;
+                    break;
+                }
+                pos += kHeaderSize + body;
+                bytes_consumed += sz;
+                skipped++;
+                continue;
+            }
+            bytes_consumed += sz;
+            if (body > avail) {
+                err = RPGPU_V_STREAM_SHORT;
+                break;
+            }
+            const uint64_t bpos = pos;
+            pos += kHeaderSize + body;
+            // consume_batch_end (:951-975)
+            if (codec > 4u) {  // record_batch(tag_ctor_ng) throws (model/record.h:582-585)
+                thrown = RPGPU_V_BAD_CODEC_THROW;
+                break;
+            }
+            cfg_bytes += sz;
+            cur_rp = last + 1;
+            if (last - delta + 1 > start_offset) start_offset = last - delta + 1;
+            if (accepted < rd.desc_cap && l == 0) {
+                rpgpu_batch_desc d;
+                d.offset = rd.offset + bpos;
+                d.length = (uint32_t)(body + kHeaderSize);
+                d.partition = rd.partition;
+                d.format = RPGPU_FMT_RP_DISK;
+                d.ops = rd.ops;
+                d.flags = 0;
+                d.reserved = 0;
+                descs[rd.desc_first + accepted] = d;
+                kafka_base[rd.desc_first + accepted] = base_offset - delta;
+            }
+            accepted++;
+            produced += sz;  // remote_segment_batch_reader::produce (:1073-1079)
+            if (over_budget || produced > kMaxConsumeSize) {
+                stopped = true;
+                break;
+            }
+        }
+        if (l == 0) {
+            rpgpu_remote_parse_result r;
+            const bool benign = err == RPGPU_V_OK || err == RPGPU_V_END_OF_STREAM || err == RPGPU_V_FALLOCATED_ZERO;
+            r.last_error = thrown != RPGPU_V_OK ? RPGPU_V_OK : err;
+            r.status = thrown != RPGPU_V_OK ? thrown : ((bytes_consumed || benign) ? RPGPU_V_OK : err);
+            r.accepted = accepted < rd.desc_cap ? accepted : rd.desc_cap;
+            r.skipped = skipped;
+            r.bytes_consumed = bytes_consumed;
+            r.start_offset = start_offset;
+            r.cfg_bytes_consumed = cfg_bytes;
+            r.cur_delta = delta;
+            r.cur_rp_offset = cur_rp;
+            r.produced_bytes = produced;
+            r.gaps = ngaps;
+            r.over_budget = over_budget;
+            r.stopped = stopped;
+            r.reserved = 0;
+            results[s] = r;
+        }
+    }
+}
+
+hipError_t launch_remote_parse(const uint8_t* d_data, const rpgpu_remote_read* d_reads, uint32_t n,
+                               rpgpu_remote_parse_result* d_res, rpgpu_batch_desc* d_descs, int64_t* d_kafka_base,
+                               int64_t* d_gaps, const uint32_t* d_tables, int grid, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t need = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+    const uint32_t g = (uint32_t)grid < need ? (uint32_t)grid : need;
+    remote_parse_kernel<<<g, kValidateThreads, 0, s>>>(d_data, d_reads, n, d_res, d_descs, d_kafka_base, d_gaps,
+                                                       d_tables);
+    return hipGetLastError();
 }
 
 hipError_t launch_segment_parse(const uint8_t* d_data, const rpgpu_segment_read* d_reads, uint32_t n,

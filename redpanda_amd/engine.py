@@ -145,7 +145,7 @@ class Engine:
         if rc != abi.RPGPU_OK:
             raise EngineError(f"rpgpu_decomp_run_device: {rc} {self.last_error()}")
 
-    def decompress_arena(self, data: np.ndarray, descs: np.ndarray) -> dict:
+    def decompress_arena(self, data: np.ndarray, descs: np.ndarray, runs: int = 1) -> dict:
         """Validate a host arena, then decompress, rewrite and walk its compressed
         batches through the device entry points (HBM buffers from torch).
         Returns host copies: results (validation), dres, out (output buffer),
@@ -180,10 +180,11 @@ class Engine:
         d_odescs = torch.zeros(m * 24, dtype=torch.uint8, device=dev)
         d_ores = torch.zeros(m * 64, dtype=torch.uint8, device=dev)
         d_index = torch.zeros(index_cap * 32, dtype=torch.uint8, device=dev)
-        self.decomp_run_device(d_descs.data_ptr(), n, d_data.data_ptr(), d_res.data_ptr(),
-                               d_dres.data_ptr(), d_out.data_ptr(), out_cap, d_odescs.data_ptr(),
-                               d_ores.data_ptr(), d_index.data_ptr(), index_cap,
-                               d_used.data_ptr() + 8, d_scr.data_ptr(), sh)
+        for _ in range(runs):  # a plan may be run any number of times
+            self.decomp_run_device(d_descs.data_ptr(), n, d_data.data_ptr(), d_res.data_ptr(),
+                                   d_dres.data_ptr(), d_out.data_ptr(), out_cap, d_odescs.data_ptr(),
+                                   d_ores.data_ptr(), d_index.data_ptr(), index_cap,
+                                   d_used.data_ptr() + 8, d_scr.data_ptr(), sh)
         torch.cuda.synchronize(dev)
         used = int(d_used[1].item())
         return dict(
@@ -341,6 +342,37 @@ class Engine:
         torch.cuda.synchronize(dev)
         return dict(results=d_res.cpu().numpy().view(abi.SEGMENT_PARSE_RESULT_DTYPE)[:n].copy(),
                     descs=d_descs.cpu().numpy().view(abi.DESC_DTYPE)[:ncap].copy())
+
+    # -- remote (tiered storage) segment reader (rpgpu_remote_segment_parse_device) --------
+    def remote_segment_parse(self, data: np.ndarray, reads: np.ndarray) -> dict:
+        """remote_segment_batch_reader::read_some over each read on the GPU.
+        Returns host copies: results, descs, kafka_base (per descriptor slot),
+        gaps ([slot, 2]: base, last)."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        reads = np.ascontiguousarray(reads, dtype=abi.REMOTE_READ_DTYPE)
+        n = len(reads)
+        ncap = int((reads["desc_first"].astype(np.int64) + reads["desc_cap"]).max()) if n else 0
+        gcap = int((reads["gap_first"].astype(np.int64) + reads["gap_cap"]).max()) if n else 0
+        sh = torch.cuda.current_stream(dev).cuda_stream
+        d_data = torch.from_numpy(data.copy()).to(dev)
+        d_reads = torch.from_numpy(reads.view(np.uint8).copy()).to(dev)
+        d_res = torch.zeros(max(n, 1) * abi.REMOTE_PARSE_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        d_descs = torch.zeros(max(ncap, 1) * 24, dtype=torch.uint8, device=dev)
+        d_kb = torch.zeros(max(ncap, 1), dtype=torch.int64, device=dev)
+        d_gaps = torch.zeros(max(gcap, 1) * 2, dtype=torch.int64, device=dev)
+        rc = self._lib.rpgpu_remote_segment_parse_device(self._ctx, d_data.data_ptr(), d_reads.data_ptr(), n,
+                                                         d_res.data_ptr(), d_descs.data_ptr(), d_kb.data_ptr(),
+                                                         d_gaps.data_ptr(), sh)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_remote_segment_parse_device: {rc} {self.last_error()}")
+        torch.cuda.synchronize(dev)
+        return dict(results=d_res.cpu().numpy().view(abi.REMOTE_PARSE_RESULT_DTYPE)[:n].copy(),
+                    descs=d_descs.cpu().numpy().view(abi.DESC_DTYPE)[:ncap].copy(),
+                    kafka_base=d_kb.cpu().numpy()[:ncap].copy(),
+                    gaps=d_gaps.cpu().numpy().reshape(-1, 2)[:gcap].copy())
 
     def compaction_keep(self, data: np.ndarray, descs: np.ndarray, results: np.ndarray,
                         index: np.ndarray) -> tuple[np.ndarray, int]:

@@ -137,7 +137,7 @@ def test_c_client_on_device(client):
     assert "abi_client gpu: ok" in r.stdout
 
 
-@pytest.mark.parametrize("parts,n", [(1, 1000), (5, 777), (4096, 20000)])
+@pytest.mark.parametrize("parts,n", [(1, 1000), (5, 777), (4096, 20000), (4096, 300000), (8192, 50000)])
 def test_partition_summaries_device(eng, parts, n):
     """rpgpu_partition_summaries_device against the numpy restatement; a
     sub-range ignores the other partitions' batches."""

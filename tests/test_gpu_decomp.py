@@ -173,7 +173,49 @@ def test_large_bodies_split_fallback(eng):
                 comp[n // 3] = 0xFF
             bs.append(batch(bytes(comp), fmt=WIRE, record_count=len(recs), attrs=codec))
     data, descs = arena(bs, fmt=WIRE, ops=OPS)
-    compare(eng.decompress_arena(data, descs), data, descs)
+    compare(eng.decompress_arena(data, descs, runs=3), data, descs)
+
+
+def test_split_parts_overflow(eng):
+    """more split parts than the part list holds ((n + 4096) / 2 per
+    codec).  320 ~1 MiB LZ4 bodies of 16 independent 64 KiB blocks each (5,120
+    parts) plus damaged and small ones: the bodies whose parts do not fit go
+    to the serial decoders; nothing decodes from a stale or unwritten part
+    record; every verdict, length and byte as the oracle's, also when the plan
+    is run three times."""
+    rng = np.random.default_rng(23)
+    recs = records(rng, 900, 8, 1100, text=True)
+    body = b"".join(recs)
+    clean = orc.compress(3, body)
+    bs = []
+    for i in range(320):
+        comp = bytearray(clean)
+        if i % 37 == 5:
+            comp[len(comp) // 2] ^= 0x5A  # a part fails: serial fallback
+        bs.append(batch(bytes(comp), fmt=WIRE, record_count=len(recs), attrs=3, base_offset=i * 1000))
+        if i % 16 == 0:  # small batches in between (lane decoders)
+            small = records(rng, 4, 4, 200, text=True)
+            bs.append(batch(orc.compress(3, b"".join(small)), fmt=WIRE, record_count=4, attrs=3))
+    data, descs = arena(bs, fmt=WIRE, ops=OPS)
+    compare(eng.decompress_arena(data, descs, runs=3), data, descs)
+
+
+def test_many_tiny_zstd_gzip(eng):
+    """more zstd / gzip batches than the engine runs decoders for
+    at once (131,072), ~100-400 B bodies, so decoders are reused across frames;
+    1 in 200 batches corrupted.  Every verdict, length, rewritten byte and
+    index entry as the oracle's."""
+    from redpanda_amd import abi, engine
+
+    spec = engine.make_spec(seed=0x5EED0077, partitions=64, codec_mix=(1 << 4) | (1 << 1), body_min=100,
+                            body_max=400, ops=abi.OPS_PRODUCE | abi.OP_DECOMP, payload=abi.PAYLOAD_TEXT,
+                            corrupt_ppm=5_000, corrupt_mask=0x3FF)
+    data, descs = engine.build_arena(spec, 150_000)
+    got = eng.decompress_arena(data, descs)
+    compare(got, data, descs)
+    v, codec = got["dres"]["verdict"], got["dres"]["codec"]
+    assert ((v == abi.V_OK) & (codec == 4)).sum() > 131_072 // 2
+    assert ((v == abi.V_OK) & (codec == 1)).sum() > 131_072 // 2
 
 
 def test_uncompress_scalar_mirror(eng):
