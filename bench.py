@@ -191,7 +191,8 @@ def full_check(spec, chunks, part_shift, res, dres, ores, index, gen_threads, pi
             for kind, diff in (
                     ("validation", np.any([res[f][sl] != r0[f] for f in names], axis=0)),
                     ("decomp_verdict", dres["verdict"][sl] != w["verdicts"]),
-                    ("decoded_len", dres["out_len"][sl] != w["out_len"]),
+                    # decoded length of the OK ones (after an error the reference keeps nothing)
+                    ("decoded_len", (dres["out_len"][sl] != w["out_len"]) & (w["verdicts"] == abi.V_OK)),
                     ("rewritten_result", np.any([ores[f][sl] != w["out_results"][f] for f in names], axis=0))):
                 kinds[kind] += int(diff.sum())
                 bad[sl] |= diff
@@ -210,6 +211,7 @@ def full_check(spec, chunks, part_shift, res, dres, ores, index, gen_threads, pi
     hist_g = {abi.VERDICT_NAMES.get(int(v), str(int(v))): int(n_)
               for v, n_ in zip(*np.unique(dres["verdict"], return_counts=True))}
     return {"batches": int(at), "mismatched_batches": int(bad.sum()), "mismatches_by_kind": kinds,
+            "first_mismatches": np.nonzero(bad)[0][:16].tolist(),
             "decompress_verdicts_gpu": hist_g, "decompress_verdicts_oracle": hist_o,
             "validation_verdicts_gpu": {abi.VERDICT_NAMES.get(int(v), str(int(v))): int(n_)
                                         for v, n_ in zip(*np.unique(res["verdict"], return_counts=True))}}

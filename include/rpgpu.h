@@ -343,7 +343,9 @@ typedef struct rpgpu_decomp_result {
                             length with bit 31 set), SKIPPED                  */
     uint32_t codec;      /* attrs & 7 of the input batch                      */
     uint64_t out_offset; /* rewritten batch in the output buffer              */
-    uint64_t out_len;    /* decompressed body bytes                           */
+    uint64_t out_len;    /* decompressed body bytes (verdict OK; unspecified
+                            after an error, where the reference throws and
+                            keeps nothing)                                    */
     uint64_t out_cap;    /* bytes reserved for the batch (header + bound of
                             the decoded size + slack)                         */
 } rpgpu_decomp_result;   /* 32 bytes */
