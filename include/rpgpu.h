@@ -404,9 +404,26 @@ int32_t rpgpu_compress_run_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_desc
 /* Synchronous scalar mirror of compression::compressor::uncompress(buf, codec)
  * on the GPU, host buffers.  Returns the verdict (>= 0) or a negative status;
  * *out_len = decompressed bytes (the size needed when the verdict is
- * RPGPU_V_DECOMP_OVERFLOW; `out` then holds the first `cap` bytes). */
+ * RPGPU_V_DECOMP_OVERFLOW; `out` then holds the first `cap` bytes).  The
+ * per-batch ceiling (opts.max_decoded_batch) applies only when `cap` is
+ * smaller than the frame's decoded-size bound: a caller that supplies the
+ * capacity gets the decode (the retry of a DECOMP_OVERFLOW batch). */
 int32_t rpgpu_uncompress(rpgpu_ctx* ctx, int32_t codec, const void* in, size_t n, void* out,
                          size_t cap, size_t* out_len);
+
+/* Retry path of the arena decompressor: a batch that
+ * validated OK but got RPGPU_V_DECOMP_OVERFLOW from rpgpu_decomp_run_device
+ * (its decoded-size bound is above opts.max_decoded_batch; dres.out_len holds
+ * the bound) is decompressed alone, as storage::internal::
+ * maybe_decompress_batch_sync does (storage/parser_utils.cc:52-68,122-128):
+ * `out` receives the rewritten on-disk batch -- the 61-byte little-endian
+ * header with the codec bits removed, size_bytes = 61 + body, fresh crc and
+ * header_crc -- followed by the body.  Size `cap` as 61 + dres.out_len.
+ * Returns the verdict (RPGPU_V_OK, a decompress error, or
+ * RPGPU_V_DECOMP_OVERFLOW with *out_len = the capacity needed) or a negative
+ * status (RPGPU_EINVAL: not a compressed batch of the given format). */
+int32_t rpgpu_decompress_batch(rpgpu_ctx* ctx, const void* batch, size_t len, int32_t format, void* out, size_t cap,
+                               size_t* out_len);
 
 /* ---- multi-batch record sets ---------------------------------------------
  * Replaces kafka::batch_reader (kafka/protocol/batch_reader.cc:50-161) over

@@ -244,6 +244,8 @@ def lib() -> C.CDLL:
              _u64, _vp, _vp, _vp)
         _sig(L.rpgpu_uncompress, _i32, _vp, _i32, _vp, C.c_size_t, _vp, C.c_size_t,
              C.POINTER(C.c_size_t))
+        _sig(L.rpgpu_decompress_batch, _i32, _vp, _vp, C.c_size_t, _i32, _vp, C.c_size_t,
+             C.POINTER(C.c_size_t))
         _sig(L.rpgpu_segment_index_device, _i32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp)
         _sig(L.rpgpu_record_sets_scratch_bytes, C.c_size_t, _u32)
         _sig(L.rpgpu_record_sets_plan_device, _i32, _vp, _vp, _u32, _vp, _vp, _vp, _vp)
@@ -280,6 +282,6 @@ EXPORTED = [
     "rpgpu_run_device", "rpgpu_crc32c_ranges_device",
     "rpgpu_crc32c_extend", "rpgpu_internal_header_only_crc", "rpgpu_crc_record_batch",
     "rpgpu_decomp_scratch_bytes", "rpgpu_decomp_plan_device", "rpgpu_decomp_run_device",
-    "rpgpu_uncompress", "rpgpu_record_sets_scratch_bytes", "rpgpu_record_sets_plan_device",
+    "rpgpu_uncompress", "rpgpu_decompress_batch", "rpgpu_record_sets_scratch_bytes", "rpgpu_record_sets_plan_device",
     "rpgpu_record_sets_run_device", "rpgpu_segment_index_device",
 ]

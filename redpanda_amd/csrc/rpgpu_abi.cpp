@@ -704,7 +704,9 @@ int32_t rpgpu_uncompress(rpgpu_ctx* c, int32_t codec, const void* in, size_t n, 
         (e = hipStreamSynchronize(c->stream)) != hipSuccess)
         return fail(c, e, "download");
     const uint64_t bound = h[0];
-    if (bound + RPGPU_HEADER_SIZE + 128 > c->max_decoded) {  // the arena path's per-batch ceiling
+    // the arena path's per-batch ceiling, unless the caller's buffer holds the
+    // bound: the retry of a DECOMP_OVERFLOW batch with out_len bytes
+    if (bound > cap && bound + RPGPU_HEADER_SIZE + 128 > c->max_decoded) {
         *out_len = bound;
         return RPGPU_V_DECOMP_OVERFLOW;
     }
@@ -727,6 +729,60 @@ int32_t rpgpu_uncompress(rpgpu_ctx* c, int32_t codec, const void* in, size_t n, 
     if (verdict == RPGPU_V_OK && len > cap) verdict = RPGPU_V_DECOMP_OVERFLOW;
     *out_len = len;
     return verdict;
+}
+
+int32_t rpgpu_decompress_batch(rpgpu_ctx* c, const void* batch, size_t len, int32_t format, void* out, size_t cap,
+                               size_t* out_len) {
+    // storage::internal::maybe_decompress_batch_sync (storage/parser_utils.cc:
+    // 52-68,122-128) for one batch the arena pass validated: decode the body
+    // (rpgpu_uncompress, bounded by the caller's buffer), then the rewritten
+    // on-disk header with fresh CRCs, exactly as finish_batch +
+    // decomp_patch_kernel write it.
+    if (!c || !batch || !out_len || (cap && !out) || len < (size_t)RPGPU_HEADER_SIZE ||
+        (format != RPGPU_FMT_KAFKA_WIRE && format != RPGPU_FMT_RP_DISK))
+        return RPGPU_EINVAL;
+    *out_len = 0;
+    const uint8_t* p = static_cast<const uint8_t*>(batch);
+    const bool be = format == RPGPU_FMT_KAFKA_WIRE;
+    auto field = [&](int off, int nb) {
+        uint64_t v = 0;
+        for (int k = 0; k < nb; k++) v = be ? (v << 8) | p[off + k] : v | ((uint64_t)p[off + k] << (8 * k));
+        return v;
+    };
+    const uint64_t size = be ? (uint64_t)(int64_t)(int32_t)field(8, 4) + 12u : (uint64_t)(uint32_t)field(4, 4);
+    if (size < (uint64_t)RPGPU_HEADER_SIZE || size > len) return RPGPU_EINVAL;
+    const int32_t codec = (int32_t)(field(21, 2) & 7);
+    if (codec < 1 || codec > 4) return RPGPU_EINVAL;
+    const size_t room = cap > (size_t)RPGPU_HEADER_SIZE ? cap - RPGPU_HEADER_SIZE : 0;
+    size_t blen = 0;
+    const int32_t v = rpgpu_uncompress(c, codec, p + RPGPU_HEADER_SIZE, size - RPGPU_HEADER_SIZE,
+                                       static_cast<uint8_t*>(out) + RPGPU_HEADER_SIZE, room, &blen);
+    if (v < 0) return v;
+    if (v != RPGPU_V_OK) {
+        *out_len = v == RPGPU_V_DECOMP_OVERFLOW ? blen + RPGPU_HEADER_SIZE : 0;
+        return v;
+    }
+    rpgpu_rp_header h;
+    memset(&h, 0, sizeof(h));
+    h.size_bytes = (int32_t)(RPGPU_HEADER_SIZE + blen);
+    h.base_offset = (int64_t)(be ? field(0, 8) : field(8, 8));
+    h.type = be ? 1 : (int8_t)p[16];  // raft_data on produce
+    h.attrs = (int16_t)(field(21, 2) & ~(uint64_t)7);
+    h.last_offset_delta = (int32_t)field(23, 4);
+    h.first_timestamp = (int64_t)field(27, 8);
+    h.max_timestamp = (int64_t)field(35, 8);
+    h.producer_id = (int64_t)field(43, 8);
+    h.producer_epoch = (int16_t)field(51, 2);
+    h.base_sequence = (int32_t)field(53, 4);
+    h.record_count = (int32_t)field(57, 4);
+    int32_t st = rpgpu_crc_record_batch(c, &h, static_cast<uint8_t*>(out) + RPGPU_HEADER_SIZE, blen, &h.crc);
+    uint32_t hc = 0;
+    if (st == RPGPU_OK) st = rpgpu_internal_header_only_crc(c, &h, &hc);
+    if (st != RPGPU_OK) return st;
+    h.header_crc = hc;
+    memcpy(out, &h, RPGPU_HEADER_SIZE);
+    *out_len = RPGPU_HEADER_SIZE + blen;
+    return RPGPU_V_OK;
 }
 
 int32_t rpgpu_crc32c_extend(rpgpu_ctx* c, uint32_t crc, const void* p, size_t n, uint32_t* out) {

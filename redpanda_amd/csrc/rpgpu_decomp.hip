@@ -136,8 +136,9 @@ constexpr uint64_t kLaneMaxSlot = 256u << 10;
 constexpr uint64_t kZstdLaneMaxSlot = RPGPU_ZSTD_LANE_MAX;  // zstd: its lane / wave boundary
 __device__ __forceinline__ uint64_t lane_max(uint32_t codec) { return codec == 4 ? kZstdLaneMaxSlot : kLaneMaxSlot; }
 
-// slot[i] of a batch whose bound exceeds the per-batch ceiling: no output
-// reserved (the scan counts 0), verdict DECOMP_OVERFLOW
+// slot[i] of a batch whose bound exceeds the per-batch ceiling: kOverCeiling |
+// bound -- no output reserved (the scan counts 0), verdict DECOMP_OVERFLOW
+// with out_len = the bound, the capacity a retry needs (rpgpu_decompress_batch)
 constexpr uint64_t kOverCeiling = 1ull << 63;
 
 __device__ __forceinline__ bool decomp_wanted(const rpgpu_batch_desc& d, const rpgpu_batch_result& v) {
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
     SplitPart* __restrict__ parts, uint32_t pcap) {
     __shared__ uint64_t wsum[kScanBlock / 64];
     const uint32_t i = blockIdx.x * kScanBlock + threadIdx.x;
-    uint64_t sz = 0;
+    uint64_t sz = 0, need = 0;
     bool over = false;
     if (i < n) {
         const rpgpu_batch_desc d = descs[i];
@@ -190,6 +191,7 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
             if (bound > max_decoded || sz > max_decoded) {
                 sz = 0;
                 over = true;
+                need = bound < kOverCeiling ? bound : kOverCeiling - 1;
             }
         }
     }
@@ -207,7 +209,7 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
     uint64_t wbase = 0;
     for (uint32_t k = 0; k < wv; k++) wbase += wsum[k];
     if (i < n) {
-        slot[i] = over ? kOverCeiling : sz;
+        slot[i] = over ? (kOverCeiling | need) : sz;
         local[i] = wbase + x - span;
         // large batches: LZ4 frames / snappy-java bodies with a split plan go
         // to the part decoders (LZ4 parts at parts[0..), snappy's at
@@ -325,9 +327,12 @@ __device__ __forceinline__ void finish_batch(uint32_t i, const rpgpu_batch_desc&
     out_descs[i] = od;
 }
 
-// the batch's output slot, or the verdict that it gets none
-__device__ __forceinline__ bool plan_slot(uint64_t& sz, uint64_t off, uint64_t out_cap, int32_t& verdict) {
-    if (sz == kOverCeiling) {
+// the batch's output slot, or the verdict that it gets none (len: the
+// capacity a retry needs when the bound is over the ceiling)
+__device__ __forceinline__ bool plan_slot(uint64_t& sz, uint64_t off, uint64_t out_cap, int32_t& verdict,
+                                          uint64_t& len) {
+    if (sz & kOverCeiling) {
+        len = sz & ~kOverCeiling;
         sz = 0;
         verdict = RPGPU_V_DECOMP_OVERFLOW;
         return false;
@@ -343,7 +348,7 @@ __device__ __forceinline__ bool plan_slot(uint64_t& sz, uint64_t off, uint64_t o
     return true;
 }
 __device__ __forceinline__ bool wave_owned(const rpgpu_batch_desc& d, const rpgpu_batch_result& v, uint64_t sz) {
-    return decomp_wanted(d, v) && sz != kOverCeiling && sz > lane_max(v.codec) && (v.codec >= 2 && v.codec <= 4);
+    return decomp_wanted(d, v) && !(sz & kOverCeiling) && sz > lane_max(v.codec) && (v.codec >= 2 && v.codec <= 4);
 }
 
 // LZ4 (CODEC 3, which also writes the verdict of every batch nobody decodes)
@@ -383,7 +388,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_
             const bool mine = want ? (v.codec == CODEC && !wave_owned(d, v, sz)) : CODEC == 3;
             if (!mine) continue;
             off = block_base[i / kScanBlock] + local[i];
-            if (want && plan_slot(sz, off, out_cap, verdict)) {
+            if (want && plan_slot(sz, off, out_cap, verdict, len)) {
                 const uint8_t* in = data + d.offset + kHeaderSize;
                 uint8_t* o = out + off + kHeaderSize;
                 const uint64_t cap = sz - kHeaderSize - rpcodec::kSlack;
@@ -422,7 +427,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_WS_WA
         const uint64_t off = block_base[i / kScanBlock] + local[i];
         int32_t verdict = RPGPU_V_SKIPPED;
         uint64_t len = 0;
-        if (plan_slot(sz, off, out_cap, verdict)) {
+        if (plan_slot(sz, off, out_cap, verdict, len)) {
             const uint8_t* in = data + d.offset + kHeaderSize;
             uint8_t* o = out + off + kHeaderSize;
             const uint64_t cap = sz - kHeaderSize - rpcodec::kSlack;
@@ -490,7 +495,7 @@ __global__ __launch_bounds__(64) void decomp_wave_kernel(
         const uint64_t off = block_base[i / kScanBlock] + local[i];
         int32_t verdict = RPGPU_V_SKIPPED;
         uint64_t len = 0;
-        if (plan_slot(sz, off, out_cap, verdict)) {
+        if (plan_slot(sz, off, out_cap, verdict, len)) {
             verdict = decode_body<FAM>(em, ws, v.codec, data + d.offset + kHeaderSize, body_len(v),
                                        out + off + kHeaderSize, sz - kHeaderSize - rpcodec::kSlack, &len);
         }
@@ -541,8 +546,8 @@ __global__ __launch_bounds__(256) void split_finish_kernel(
     const uint64_t off = block_base[i / kScanBlock] + local[i];
     int32_t verdict = RPGPU_V_OK;
     uint64_t len = 0;
-    if (!plan_slot(sz, off, out_cap, verdict)) {
-        finish_batch(i, d, v, off, sz, verdict, 0, data, out, dres, out_descs);
+    if (!plan_slot(sz, off, out_cap, verdict, len)) {
+        finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
         return;
     }
     const uint32_t f = sfirst[i];

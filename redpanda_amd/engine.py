@@ -485,7 +485,20 @@ class Engine:
                                        out.ctypes.data, cap, C.byref(n))
         if v < 0:
             raise EngineError(f"rpgpu_uncompress: {v} {self.last_error()}")
+        self.last_out_len = int(n.value)  # the capacity needed after RPGPU_V_DECOMP_OVERFLOW
         return int(v), out[: min(n.value, cap)].tobytes()
+
+    def decompress_batch(self, batch: bytes, fmt: int, cap: int) -> tuple[int, bytes, int]:
+        """rpgpu_decompress_batch: the retry of a DECOMP_OVERFLOW batch.
+        Returns (verdict, rewritten on-disk batch, out_len)."""
+        a = np.ascontiguousarray(np.frombuffer(bytes(batch), dtype=np.uint8))
+        out = np.zeros(max(cap, 1), dtype=np.uint8)
+        n = C.c_size_t()
+        v = self._lib.rpgpu_decompress_batch(self._ctx, a.ctypes.data, a.size, fmt, out.ctypes.data, cap,
+                                             C.byref(n))
+        if v < 0:
+            raise EngineError(f"rpgpu_decompress_batch: {v} {self.last_error()}")
+        return int(v), out[: min(n.value, cap)].tobytes(), int(n.value)
     def crc32c_extend(self, crc: int, data: bytes | np.ndarray) -> int:
         buf = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
         buf = np.ascontiguousarray(buf, dtype=np.uint8)

@@ -299,13 +299,58 @@ def test_decoded_size_ceiling(built):
         want = compare(e.decompress_arena(data2, descs2), data2, descs2)
         assert np.array_equal(v[keep], want["verdicts"])
         assert np.array_equal(got["dres"]["out_len"][keep], want["out_len"])
-        # the scalar mirror applies the same ceiling
-        gv, _ = e.uncompress(4, hostile, cap=16 << 20)
-        assert gv == abi.V_DECOMP_OVERFLOW
+        # the arena reports the capacity a retry needs (the frame's bound)
+        need = int(got["dres"]["out_len"][2])
+        assert need >= 8 << 20
+        # the scalar mirror applies the same ceiling to a caller buffer below the bound ...
+        gv, _ = e.uncompress(4, hostile, cap=1 << 20)
+        assert gv == abi.V_DECOMP_OVERFLOW and e.last_out_len == need
+        # ... and decodes when the caller supplies the capacity (the retry)
+        gv, gout = e.uncompress(4, hostile, cap=need)
+        ov, oout = orc.uncompress(4, hostile, cap=16 << 20)
+        assert gv == ov == abi.V_OK and gout == oout
     # under the default ceiling the same frame decodes, as the oracle does
     gv, gout = eng_default_uncompress(hostile)
-    ov, oout = orc.uncompress(4, hostile, cap=16 << 20)
     assert gv == ov == abi.V_OK and gout == oout
+
+
+def test_overflow_retry_80mib(eng):
+    """DECOMP_OVERFLOW is a retry signal, not a rejection.  A valid
+    zstd frame decoding to 80 MiB (above the default 64 MiB per-batch ceiling)
+    gets no slot in the arena pass and reports the capacity it needs;
+    rpgpu_decompress_batch then rewrites it exactly as the oracle's
+    maybe_decompress_batch_sync does (rewritten header with fresh CRCs + body)."""
+    from redpanda_amd import abi
+
+    rng = np.random.default_rng(80)
+    words = [b"kafka ", b"redpanda ", b"offset ", b"batch ", b"segment ", b"raft ", b"log ", b"term "]
+    chunk = b"".join(words[k] for k in rng.integers(0, len(words), 40_000))
+    body = (chunk * (80 * (1 << 20) // len(chunk) + 1))[:80 << 20]
+    big = batch(orc.compress(4, body), fmt=WIRE, record_count=0, attrs=4, base_offset=77)
+    small = [batch(orc.compress(c, b"".join(records(rng, 10, 4, 300, text=True))), fmt=WIRE, record_count=10,
+                   attrs=c) for c in (3, 4)]
+    bs = [small[0], big, small[1]]
+    data, descs = arena(bs, fmt=WIRE, ops=OPS)
+    got = eng.decompress_arena(data, descs)
+    v = got["dres"]["verdict"]
+    assert v[1] == abi.V_DECOMP_OVERFLOW and got["dres"]["out_cap"][1] == 0
+    assert v[0] == v[2] == abi.V_OK
+    need = int(got["dres"]["out_len"][1])
+    assert need >= 80 << 20
+    gv, gout, glen = eng.decompress_batch(big, WIRE, cap=61 + need)
+    assert gv == abi.V_OK and glen == 61 + (80 << 20)
+    # the oracle's rewrite of the same batch, given the room
+    d1 = descs[1:2].copy()
+    d1["offset"] = 0
+    one = np.frombuffer(big + bytes(64), dtype=np.uint8).copy()
+    wres, _, _ = orc.validate_arena(one, d1)
+    want = orc.decompress_arena(one, d1, wres, np.array([need], dtype=np.uint64))
+    assert want["verdicts"][0] == abi.V_OK
+    o = int(want["out_descs"]["offset"][0])
+    assert gout == want["out"][o:o + glen].tobytes()
+    # a buffer too small: the retry reports the capacity again
+    gv, _, glen = eng.decompress_batch(big, WIRE, cap=1 << 20)
+    assert gv == abi.V_DECOMP_OVERFLOW and glen >= 61 + (80 << 20)
 
 
 def eng_default_uncompress(frame):
