@@ -662,14 +662,75 @@ int32_t rpgpu_partition_summaries_device(rpgpu_ctx* ctx, const rpgpu_batch_desc*
  * the index_cap index entries: 1 keep, 0 superseded by a later record with the
  * same key, 2 not a record of an OK batch (slack between batch slices, failed
  * batches).  *d_nkeys = distinct keys over all scopes.  The key map here is
- * unbounded; the reference evicts entries past its memory budget
- * (spill_key_index.cc:99-138), which can only keep more records.
+ * unbounded: parity with the reference holds only while its maps stay under
+ * their memory budgets (spill_key_index.cc:99-138; compaction_key_reducer,
+ * compaction_reducers.cc:49-67).  Past them the reference evicts entries in
+ * its hash map's iteration order and keeps the evicted keys' records as well,
+ * which this engine does not reproduce (it can only keep fewer records).
  * d_scratch: rpgpu_compaction_scratch_bytes(index_cap) bytes. */
 size_t rpgpu_compaction_scratch_bytes(uint64_t index_cap);
 int32_t rpgpu_compaction_keep_device(rpgpu_ctx* ctx, const uint8_t* d_data, const rpgpu_batch_desc* d_descs,
                                      const rpgpu_batch_result* d_results, uint32_t n,
                                      const rpgpu_record_index* d_index, uint64_t index_cap, uint8_t* d_keep,
                                      uint64_t* d_nkeys, void* d_scratch, void* hip_stream);
+
+/* ---- compaction rewrite ----------------------------------
+ * copy_data_segment_reducer::filter (storage/compaction_reducers.cc:117-251)
+ * over the batches whose records rpgpu_compaction_keep_device classified:
+ *   - a batch that did not validate OK, or whose index slice does not hold
+ *     all its records, is not rewritten (SKIPPED, no output);
+ *   - a raft_configuration / archival_metadata / version_fence batch is kept
+ *     whole (NOT_COMPACTIBLE, :119-123);
+ *   - a transactional, non-control batch loses its transactional bit (:125-143);
+ *   - no record kept: the batch is dropped (DROPPED, std::nullopt :155-158);
+ *   - every record kept: the batch as it is (KEPT; TX_CLEARED when its bit was
+ *     cleared, with fresh CRCs, :160-167);
+ *   - otherwise the kept records are re-encoded (model::append_record_to_buffer,
+ *     model/record_utils.cc:183-225: canonical varints of the parsed fields --
+ *     record size, 32-bit offset delta, key / value / header sizes -- the
+ *     bytes the parser copied, every header of the record's count), first_ts =
+ *     first_ts + the first kept record's ts delta, max_ts (create-time batches)
+ *     = that new first_ts + the last kept record's ts delta, record_count = the
+ *     kept records, then reset_size_checksum_metadata (FILTERED, :169-251).
+ * Every output is an on-disk (little-endian) batch at out_offset with fresh
+ * crc / header_crc, walked and indexed (d_out_results, d_out_index) like the
+ * rewritten batches of rpgpu_decomp_run_device.  Recompressing an originally
+ * compressed batch (do_compaction's compress_batch, :253-284) is
+ * rpgpu_compress_plan_device / run_device over the output.
+ * Plan, then run, on the same stream: the plan sizes the output
+ * (*d_out_bytes); keep is rpgpu_compaction_keep_device's d_keep. */
+enum rpgpu_compact_action {
+    RPGPU_COMPACT_SKIPPED = 0,
+    RPGPU_COMPACT_DROPPED = 1,
+    RPGPU_COMPACT_KEPT = 2,
+    RPGPU_COMPACT_TX_CLEARED = 3,
+    RPGPU_COMPACT_FILTERED = 4,
+    RPGPU_COMPACT_NOT_COMPACTIBLE = 5,
+};
+
+typedef struct rpgpu_compact_result {
+    int32_t action;        /* enum rpgpu_compact_action                       */
+    int32_t record_count;  /* records of the output batch                     */
+    uint64_t out_offset;   /* output batch in d_out                           */
+    uint64_t out_len;      /* its bytes (61 + body); 0 without an output      */
+    uint32_t removed;      /* records dropped from the batch                  */
+    uint32_t reserved;
+} rpgpu_compact_result;    /* 32 bytes */
+
+size_t rpgpu_compaction_rewrite_scratch_bytes(uint32_t n);
+int32_t rpgpu_compaction_rewrite_plan_device(rpgpu_ctx* ctx, const uint8_t* d_data, const rpgpu_batch_desc* d_descs,
+                                             const rpgpu_batch_result* d_results, uint32_t n,
+                                             const rpgpu_record_index* d_index, uint64_t index_cap,
+                                             const uint8_t* d_keep, uint64_t* d_out_bytes, void* d_scratch,
+                                             void* hip_stream);
+int32_t rpgpu_compaction_rewrite_run_device(rpgpu_ctx* ctx, const uint8_t* d_data, const rpgpu_batch_desc* d_descs,
+                                            const rpgpu_batch_result* d_results, uint32_t n,
+                                            const rpgpu_record_index* d_index, uint64_t index_cap,
+                                            const uint8_t* d_keep, rpgpu_compact_result* d_cres, uint8_t* d_out,
+                                            uint64_t out_cap, rpgpu_batch_desc* d_out_descs,
+                                            rpgpu_batch_result* d_out_results, rpgpu_record_index* d_out_index,
+                                            uint64_t out_index_cap, uint64_t* d_out_index_used, void* d_scratch,
+                                            void* hip_stream);
 
 /* ---- fetch serialization ----------------------------------
  * kafka_batch_serializer (kafka/protocol/batch_consumer.h:26-101) over batches a

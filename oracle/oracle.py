@@ -97,6 +97,8 @@ def lib() -> C.CDLL:
         L.orc_decompress_batches.argtypes = [vp, u32, vp, vp, u32, vp, vp, vp, vp, vp, vp, C.c_int]
         L.orc_compaction_keep.restype = None
         L.orc_compaction_keep.argtypes = [vp, vp, vp, u32, vp, u64, vp, C.POINTER(u64)]
+        L.orc_compact_rewrite.restype = u64
+        L.orc_compact_rewrite.argtypes = [vp, vp, vp, u32, vp, u64, vp, vp, vp, vp]
         L.orc_batch_timequery.restype = None
         L.orc_batch_timequery.argtypes = [vp, u32, vp, vp, u32, vp]
         L.orc_kafka_serialize.restype = None
@@ -299,6 +301,31 @@ def compaction_keep(data: np.ndarray, descs: np.ndarray, results: np.ndarray, in
     lib().orc_compaction_keep(data.ctypes.data, descs.ctypes.data, results.ctypes.data, len(descs),
                               index.ctypes.data, len(index), keep.ctypes.data, C.byref(nkeys))
     return keep[: len(index)], nkeys.value
+
+
+def compaction_rewrite(data: np.ndarray, descs: np.ndarray, results: np.ndarray, index: np.ndarray,
+                       keep: np.ndarray) -> dict:
+    """copy_data_segment_reducer::filter per batch (oracle/compact.c), then the
+    output batches validated and indexed: dict(cres, out, out_descs,
+    out_results, index, used, out_bytes)."""
+    from redpanda_amd.abi import COMPACT_RESULT_DTYPE, INDEX_DTYPE
+
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    descs = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+    results = np.ascontiguousarray(results, dtype=RESULT_DTYPE)
+    index = np.ascontiguousarray(index, dtype=INDEX_DTYPE)
+    keep = np.ascontiguousarray(keep, dtype=np.uint8)
+    n = len(descs)
+    cres = np.zeros(max(n, 1), dtype=COMPACT_RESULT_DTYPE)
+    odescs = np.zeros(max(n, 1), dtype=DESC_DTYPE)
+    args = (data.ctypes.data, descs.ctypes.data, results.ctypes.data, n, index.ctypes.data, len(index),
+            keep.ctypes.data)
+    total = lib().orc_compact_rewrite(*args, None, cres.ctypes.data, odescs.ctypes.data)
+    out = np.zeros(int(total) + 64, dtype=np.uint8)
+    lib().orc_compact_rewrite(*args, out.ctypes.data, cres.ctypes.data, odescs.ctypes.data)
+    rres, ridx, rused = validate_arena(out, odescs[:n])
+    return dict(cres=cres[:n], out=out, out_descs=odescs[:n], out_results=rres, index=ridx, used=rused,
+                out_bytes=int(total))
 
 
 def batch_timequery(results: np.ndarray, index: np.ndarray, queries: np.ndarray) -> np.ndarray:

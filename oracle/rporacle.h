@@ -127,6 +127,11 @@ void orc_remote_segment_parse(const uint8_t* data, const rpgpu_remote_read* rd, 
 void orc_compaction_keep(const uint8_t* data, const rpgpu_batch_desc* descs, const rpgpu_batch_result* res,
                          uint32_t n, const rpgpu_record_index* index, uint64_t index_cap, uint8_t* keep,
                          uint64_t* nkeys);
+/* copy_data_segment_reducer::filter (compaction_reducers.cc:117-251) per
+ * batch; out == NULL sizes only.  Returns the bytes of all output slots. */
+uint64_t orc_compact_rewrite(const uint8_t* data, const rpgpu_batch_desc* descs, const rpgpu_batch_result* res,
+                             uint32_t n, const rpgpu_record_index* index, uint64_t index_cap, const uint8_t* keep,
+                             uint8_t* out, rpgpu_compact_result* cres, rpgpu_batch_desc* odescs);
 void orc_batch_timequery(const rpgpu_batch_result* res, uint32_t n, const rpgpu_record_index* index,
                          const rpgpu_timequery* q, uint32_t nq, rpgpu_timequery_result* out);
 

@@ -126,6 +126,10 @@ REMOTE_PARSE_RESULT_DTYPE = np.dtype([("status", "<i4"), ("last_error", "<i4"), 
                                       ("cfg_bytes_consumed", "<u8"), ("cur_delta", "<i8"), ("cur_rp_offset", "<i8"),
                                       ("produced_bytes", "<u8"), ("gaps", "<u4"), ("over_budget", "u1"),
                                       ("stopped", "u1"), ("reserved", "<u2")])
+COMPACT_RESULT_DTYPE = np.dtype([("action", "<i4"), ("record_count", "<i4"), ("out_offset", "<u8"),
+                                 ("out_len", "<u8"), ("removed", "<u4"), ("reserved", "<u4")])
+assert COMPACT_RESULT_DTYPE.itemsize == 32
+COMPACT_SKIPPED, COMPACT_DROPPED, COMPACT_KEPT, COMPACT_TX_CLEARED, COMPACT_FILTERED, COMPACT_NOT_COMPACTIBLE = range(6)
 assert REMOTE_READ_DTYPE.itemsize == 96 and REMOTE_PARSE_RESULT_DTYPE.itemsize == 72
 TIMEQUERY_DTYPE = np.dtype([("batch", "<u4"), ("reserved", "<u4"), ("time", "<i8")])
 TIMEQUERY_RESULT_DTYPE = np.dtype([("offset", "<i8"), ("time", "<i8"), ("status", "<i4"), ("reserved", "<u4")])
@@ -230,6 +234,10 @@ def lib() -> C.CDLL:
         _sig(L.rpgpu_partition_summaries_device, _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
         _sig(L.rpgpu_compaction_scratch_bytes, C.c_size_t, _u64)
         _sig(L.rpgpu_compaction_keep_device, _i32, _vp, _vp, _vp, _vp, _u32, _vp, _u64, _vp, _vp, _vp, _vp)
+        _sig(L.rpgpu_compaction_rewrite_scratch_bytes, C.c_size_t, _u32)
+        _sig(L.rpgpu_compaction_rewrite_plan_device, _i32, _vp, _vp, _vp, _vp, _u32, _vp, _u64, _vp, _vp, _vp, _vp)
+        _sig(L.rpgpu_compaction_rewrite_run_device, _i32, _vp, _vp, _vp, _vp, _u32, _vp, _u64, _vp, _vp, _vp, _u64,
+             _vp, _vp, _vp, _u64, _vp, _vp, _vp)
         _sig(L.rpgpu_batch_timequery_device, _i32, _vp, _vp, _u32, _vp, _vp, _u32, _vp, _vp)
         _sig(L.rpgpu_kafka_serialize_device, _i32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _u32, _vp, _vp)
         _sig(L.rpgpu_compress_scratch_bytes, C.c_size_t, _u32)
@@ -275,7 +283,8 @@ EXPORTED = [
     "rpgpu_arena_alloc", "rpgpu_arena_free", "rpgpu_submit", "rpgpu_poll", "rpgpu_wait",
     "rpgpu_eventfd", "rpgpu_kafka_error_code", "rpgpu_kafka_error_codes_device",
     "rpgpu_partition_summaries_device", "rpgpu_segment_parse_device", "rpgpu_remote_segment_parse_device",
-    "rpgpu_compaction_scratch_bytes", "rpgpu_compaction_keep_device", "rpgpu_batch_timequery_device",
+    "rpgpu_compaction_scratch_bytes", "rpgpu_compaction_keep_device", "rpgpu_compaction_rewrite_scratch_bytes",
+    "rpgpu_compaction_rewrite_plan_device", "rpgpu_compaction_rewrite_run_device", "rpgpu_batch_timequery_device",
     "rpgpu_kafka_serialize_device", "rpgpu_compress_scratch_bytes", "rpgpu_compress_plan_device",
     "rpgpu_compress_run_device",
     "rpgpu_validate_scratch_bytes", "rpgpu_validate_device", "rpgpu_plan_device",

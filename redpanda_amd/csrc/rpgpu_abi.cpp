@@ -75,6 +75,16 @@ hipError_t launch_summaries(const rpgpu_batch_desc* d_descs, const rpgpu_batch_r
                             int cu_count);
 size_t summary_scratch_bytes(int cu_count);
 size_t compaction_scratch_bytes(uint64_t index_cap);
+size_t compaction_rewrite_scratch_bytes(uint32_t n);
+hipError_t launch_compact_rw_plan(const uint8_t* d_data, const rpgpu_batch_desc* d_descs,
+                                  const rpgpu_batch_result* d_res, uint32_t n, uint64_t index_cap,
+                                  const uint8_t* d_keep, uint64_t* d_out_bytes, void* d_scratch, hipStream_t s);
+hipError_t launch_compact_rw_run(const uint8_t* d_data, const rpgpu_batch_desc* d_descs,
+                                 const rpgpu_batch_result* d_res, uint32_t n, const uint8_t* d_keep,
+                                 rpgpu_compact_result* d_cres, uint8_t* d_out, uint64_t out_cap,
+                                 rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_out_res,
+                                 rpgpu_record_index* d_out_index, uint64_t out_index_cap, uint64_t* d_out_index_used,
+                                 void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s);
 hipError_t launch_compaction_keep(const uint8_t* d_data, const rpgpu_batch_desc* d_descs,
                                   const rpgpu_batch_result* d_res, uint32_t n, const rpgpu_record_index* d_index,
                                   uint64_t index_cap, uint8_t* d_keep, uint64_t* d_nkeys, void* d_scratch,
@@ -320,6 +330,43 @@ int32_t rpgpu_partition_summaries_device(rpgpu_ctx* c, const rpgpu_batch_desc* d
 }
 
 size_t rpgpu_compaction_scratch_bytes(uint64_t index_cap) { return rpgpu::compaction_scratch_bytes(index_cap); }
+
+size_t rpgpu_compaction_rewrite_scratch_bytes(uint32_t n) { return rpgpu::compaction_rewrite_scratch_bytes(n); }
+
+int32_t rpgpu_compaction_rewrite_plan_device(rpgpu_ctx* c, const uint8_t* d_data, const rpgpu_batch_desc* d_descs,
+                                             const rpgpu_batch_result* d_results, uint32_t n,
+                                             const rpgpu_record_index* d_index, uint64_t index_cap,
+                                             const uint8_t* d_keep, uint64_t* d_out_bytes, void* d_scratch,
+                                             void* hip_stream) {
+    (void)d_index;  // the keep flags are per index entry; the walk re-reads the records
+    if (!c || (n && (!d_data || !d_descs || !d_results || !d_keep || !d_scratch))) return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_compact_rw_plan(d_data, d_descs, d_results, n, index_cap, d_keep, d_out_bytes,
+                                                 d_scratch, s);
+    if (e != hipSuccess) return fail(c, e, "compaction rewrite plan launch");
+    return RPGPU_OK;
+}
+
+int32_t rpgpu_compaction_rewrite_run_device(rpgpu_ctx* c, const uint8_t* d_data, const rpgpu_batch_desc* d_descs,
+                                            const rpgpu_batch_result* d_results, uint32_t n,
+                                            const rpgpu_record_index* d_index, uint64_t index_cap,
+                                            const uint8_t* d_keep, rpgpu_compact_result* d_cres, uint8_t* d_out,
+                                            uint64_t out_cap, rpgpu_batch_desc* d_out_descs,
+                                            rpgpu_batch_result* d_out_results, rpgpu_record_index* d_out_index,
+                                            uint64_t out_index_cap, uint64_t* d_out_index_used, void* d_scratch,
+                                            void* hip_stream) {
+    (void)d_index;
+    (void)index_cap;
+    if (!c || (n && (!d_data || !d_descs || !d_results || !d_keep || !d_cres || !d_out || !d_out_descs ||
+                     !d_out_results || !d_scratch)))
+        return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_compact_rw_run(d_data, d_descs, d_results, n, d_keep, d_cres, d_out, out_cap,
+                                                d_out_descs, d_out_results, d_out_index, out_index_cap,
+                                                d_out_index_used, d_scratch, c->d_tables, c->grid, s);
+    if (e != hipSuccess) return fail(c, e, "compaction rewrite run launch");
+    return RPGPU_OK;
+}
 
 int32_t rpgpu_compaction_keep_device(rpgpu_ctx* c, const uint8_t* d_data, const rpgpu_batch_desc* d_descs,
                                      const rpgpu_batch_result* d_results, uint32_t n,

@@ -374,6 +374,64 @@ class Engine:
                     kafka_base=d_kb.cpu().numpy()[:ncap].copy(),
                     gaps=d_gaps.cpu().numpy().reshape(-1, 2)[:gcap].copy())
 
+    # -- compaction rewrite (rpgpu_compaction_rewrite_plan_device / run_device) ------------
+    def compaction_rewrite(self, data: np.ndarray, descs: np.ndarray, results: np.ndarray, index: np.ndarray,
+                           keep: np.ndarray) -> dict:
+        """copy_data_segment_reducer::filter over a validated, indexed arena and
+        its keep flags, on the GPU.  Returns host copies: cres, out, out_descs,
+        out_results, index, used, out_bytes."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        descs = np.ascontiguousarray(descs, dtype=abi.DESC_DTYPE)
+        results = np.ascontiguousarray(results, dtype=abi.RESULT_DTYPE)
+        index = np.ascontiguousarray(index, dtype=abi.INDEX_DTYPE)
+        keep = np.ascontiguousarray(keep, dtype=np.uint8)
+        n, m = len(descs), max(len(descs), 1)
+        sh = torch.cuda.current_stream(dev).cuda_stream
+
+        def up(a):
+            return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).to(dev)
+
+        d_data, d_descs, d_res = up(data), up(descs), up(results)
+        d_index = up(index) if len(index) else torch.zeros(32, dtype=torch.uint8, device=dev)
+        d_keep = up(keep) if len(keep) else torch.zeros(1, dtype=torch.uint8, device=dev)
+        d_scr = torch.zeros(max(int(self._lib.rpgpu_compaction_rewrite_scratch_bytes(n)), 1), dtype=torch.uint8,
+                            device=dev)
+        d_used = torch.zeros(2, dtype=torch.int64, device=dev)
+        rc = self._lib.rpgpu_compaction_rewrite_plan_device(self._ctx, d_data.data_ptr(), d_descs.data_ptr(),
+                                                            d_res.data_ptr(), n, d_index.data_ptr(), len(index),
+                                                            d_keep.data_ptr(), d_used.data_ptr(), d_scr.data_ptr(),
+                                                            sh)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_compaction_rewrite_plan_device: {rc} {self.last_error()}")
+        torch.cuda.synchronize(dev)
+        out_bytes = int(d_used[0].item())
+        out_cap = out_bytes + abi.ARENA_TAIL_PAD
+        index_cap = int(np.maximum(results["record_count"], 0).astype(np.int64).sum()) + 1
+        d_out = torch.zeros(out_cap, dtype=torch.uint8, device=dev)
+        d_cres = torch.zeros(m * abi.COMPACT_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        d_odescs = torch.zeros(m * 24, dtype=torch.uint8, device=dev)
+        d_ores = torch.zeros(m * 64, dtype=torch.uint8, device=dev)
+        d_oidx = torch.zeros(index_cap * 32, dtype=torch.uint8, device=dev)
+        rc = self._lib.rpgpu_compaction_rewrite_run_device(self._ctx, d_data.data_ptr(), d_descs.data_ptr(),
+                                                           d_res.data_ptr(), n, d_index.data_ptr(), len(index),
+                                                           d_keep.data_ptr(), d_cres.data_ptr(), d_out.data_ptr(),
+                                                           out_cap, d_odescs.data_ptr(), d_ores.data_ptr(),
+                                                           d_oidx.data_ptr(), index_cap, d_used.data_ptr() + 8,
+                                                           d_scr.data_ptr(), sh)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_compaction_rewrite_run_device: {rc} {self.last_error()}")
+        torch.cuda.synchronize(dev)
+        used = int(d_used[1].item())
+        return dict(cres=d_cres.cpu().numpy().view(abi.COMPACT_RESULT_DTYPE)[:n].copy(),
+                    out=d_out.cpu().numpy(),
+                    out_descs=d_odescs.cpu().numpy().view(abi.DESC_DTYPE)[:n].copy(),
+                    out_results=d_ores.cpu().numpy().view(abi.RESULT_DTYPE)[:n].copy(),
+                    index=d_oidx.cpu().numpy().view(abi.INDEX_DTYPE)[:min(used, index_cap)].copy(),
+                    used=used, out_bytes=out_bytes)
+
     def compaction_keep(self, data: np.ndarray, descs: np.ndarray, results: np.ndarray,
                         index: np.ndarray) -> tuple[np.ndarray, int]:
         """rpgpu_compaction_keep_device over a validated + indexed arena (host

@@ -266,3 +266,192 @@ def test_gpu_batch_timequery_random(eng):
     got = eng.batch_timequery(res, idx, q)
     want = orc.batch_timequery(res, idx, q)
     assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+
+
+# ---- compaction rewrite: copy_data_segment_reducer::filter -----------------------------
+
+def _rv(b, pos):
+    """utils/vint.h read (<= 10 bytes, partial at the end of input), zigzag."""
+    res, shift, k = 0, 0, pos
+    while k < len(b):
+        if shift > 63:
+            break
+        x = b[k]
+        k += 1
+        res |= (x & 127) << shift
+        if not x & 128:
+            break
+        shift += 7
+    res &= (1 << 64) - 1
+    v = (res >> 1) ^ (-(res & 1) & ((1 << 64) - 1))
+    return (v - (1 << 64) if v >> 63 else v), k
+
+
+def _wv(v):
+    z = ((v << 1) ^ (v >> 63)) & ((1 << 64) - 1)
+    out = bytearray()
+    while z >= 0x80:
+        out.append((z & 0x7F) | 0x80)
+        z >>= 7
+    out.append(z)
+    return bytes(out)
+
+
+def _i32(v):
+    v &= 0xFFFFFFFF
+    return v - (1 << 32) if v >> 31 else v
+
+
+def python_filter(body: bytes, rc: int, keep_flags) -> tuple[bytes, int, int]:
+    """filter() steps 1 and 4 with append_record_to_buffer (record_utils.cc:
+    183-225): (re-encoded kept records, first kept ts delta, last kept ts delta)."""
+    pos, out, first, last = 0, bytearray(), None, None
+    for j in range(rc):
+        size, pos = _rv(body, pos)
+        attrs = body[pos]
+        pos += 1
+        ts, pos = _rv(body, pos)
+        off, pos = _rv(body, pos)
+        kl, pos = _rv(body, pos)
+        key = body[pos:pos + kl] if kl > 0 else b""
+        pos += len(key)
+        vl, pos = _rv(body, pos)
+        val = body[pos:pos + vl] if vl > 0 else b""
+        pos += len(val)
+        hc, pos = _rv(body, pos)
+        hdrs = []
+        for _ in range(hc):
+            hk, pos = _rv(body, pos) if pos < len(body) else (0, pos)
+            hkb = body[pos:pos + hk] if hk > 0 else b""
+            pos += len(hkb)
+            hv, pos = _rv(body, pos) if pos < len(body) else (0, pos)
+            hvb = body[pos:pos + hv] if hv > 0 else b""
+            pos += len(hvb)
+            hdrs.append((_i32(hk), hkb, _i32(hv), hvb))
+        if keep_flags[j] != 1:
+            continue
+        first = ts if first is None else first
+        last = ts
+        out += _wv(_i32(size)) + bytes([attrs]) + _wv(ts) + _wv(_i32(off))
+        out += _wv(_i32(kl)) + (key if _i32(kl) > 0 else b"") + _wv(_i32(vl)) + (val if _i32(vl) > 0 else b"")
+        out += _wv(len(hdrs))
+        for hk, hkb, hv, hvb in hdrs:
+            out += _wv(hk) + (hkb if hk > 0 else b"") + _wv(hv) + (hvb if hv > 0 else b"")
+    return bytes(out), first, last
+
+
+def rewrite_arena(seed, nb=150, fmt=DISK):
+    """keyed_arena plus transactional / control / append-time batches,
+    headers (some past the end of a truncated last record) and non-canonical
+    varints, so every branch of filter() is taken."""
+    rng = np.random.default_rng(seed)
+    keys = [None, b"", b"a", b"b", b"key-1", b"key-2", b"k" * 40]
+    bs, off = [], 0
+    for i in range(nb):
+        nrec = int(rng.integers(1, 10))
+        recs = []
+        for j in range(nrec):
+            hdrs = [(b"h%d" % h, b"x" * int(rng.integers(0, 4))) for h in range(int(rng.integers(0, 3)))]
+            r = record(keys[int(rng.integers(0, len(keys)))], b"v%d" % j if rng.random() > 0.1 else None,
+                       ts_delta=int(rng.integers(0, 50)), off_delta=j, headers=hdrs,
+                       attrs=int(rng.integers(0, 3)))
+            if rng.random() < 0.05:  # a padded (non-canonical) record-size varint
+                size, k = _rv(r, 0)
+                r = bytes([r[0] | 0x80, 0x00]) + r[1:] if r[0] < 0x80 else r
+            recs.append(r)
+        body = b"".join(recs)
+        if i % 17 == 3:  # the last record declares 4 headers but the body ends after its count
+            body += record(b"a", b"z", ts_delta=1, off_delta=nrec, hcount=4)
+            nrec += 1
+        attrs = int(rng.choice([0, 0, 0x10, 0x30, 0x08, 0x18]))
+        bt = int(rng.choice([1, 1, 1, 1, 2, 19, 23, 5])) if fmt == DISK else 1
+        bs.append(batch(body, fmt=fmt, base_offset=off, btype=bt, attrs=attrs, record_count=nrec,
+                        first_ts=1_700_000_000_000 + i, max_ts=1_700_000_000_000 + i + 1000))
+        off += nrec
+    return arena(bs, fmt=fmt, ops=abi.OPS_PRODUCE)
+
+
+def python_rewrite_check(data, descs, res, idx, keep, got):
+    """Every batch's action and output bytes against python_filter."""
+    import struct
+
+    cres = got["cres"]
+    seen = set()
+    for b in range(len(descs)):
+        r, c = res[b], cres[b]
+        if r["verdict"] != 0:
+            assert c["action"] == abi.COMPACT_SKIPPED
+            continue
+        lo, cnt = int(r["index_first"]), int(r["index_count"])
+        k = keep[lo:lo + cnt]
+        p = int(descs["offset"][b])
+        body = data[p + 61:p + int(r["size_bytes"])].tobytes()
+        attrs = int(r["attrs"]) & 0xFFFF
+        if int(r["type"]) in NON_COMPACTIBLE:
+            want_action, want_body = abi.COMPACT_NOT_COMPACTIBLE, body
+        else:
+            tx = (attrs & 0x10) and not (attrs & 0x20)
+            if tx:
+                attrs &= ~0x10
+            if (k == 1).sum() == 0:
+                assert c["action"] == abi.COMPACT_DROPPED and c["out_len"] == 0
+                continue
+            if (k == 1).all():
+                want_action, want_body = (abi.COMPACT_TX_CLEARED if tx else abi.COMPACT_KEPT), body
+            else:
+                want_action = abi.COMPACT_FILTERED
+                want_body, first, last = python_filter(body, int(r["record_count"]), k)
+        seen.add(want_action)
+        assert c["action"] == want_action, (b, c["action"], want_action)
+        o = int(c["out_offset"])
+        out = got["out"][o:o + int(c["out_len"])].tobytes()
+        assert out[61:] == want_body, b
+        h = np.frombuffer(out[:61], dtype=abi.RP_HEADER_DTYPE)[0]
+        assert int(h["attrs"]) & 0xFFFF == attrs and int(h["base_offset"]) == int(r["base_offset"])
+        if want_action == abi.COMPACT_FILTERED:
+            ft = int(r["first_timestamp"]) + first
+            assert int(h["first_timestamp"]) == ft and int(h["record_count"]) == int((k == 1).sum())
+            mt = ft + last if not attrs & 0x08 else int(r["max_timestamp"])  # the reference's max rule
+            assert int(h["max_timestamp"]) == mt
+        assert int(h["header_crc"]) == orc.internal_header_only_crc(np.frombuffer(out[:61], dtype=abi.RP_HEADER_DTYPE))
+        be40 = struct.pack(">hiqqqhii", int(h["attrs"]), int(h["last_offset_delta"]), int(h["first_timestamp"]),
+                           int(h["max_timestamp"]), int(h["producer_id"]), int(h["producer_epoch"]),
+                           int(h["base_sequence"]), int(h["record_count"]))
+        assert (int(h["crc"]) & 0xFFFFFFFF) == orc.crc32c(be40 + out[61:])
+    return seen
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+@pytest.mark.parametrize("fmt", [DISK, WIRE])
+def test_oracle_rewrite_matches_restatement(seed, fmt):
+    data, descs = rewrite_arena(seed, fmt=fmt)
+    res, idx, _ = orc.validate_arena(data, descs)
+    keep, _ = orc.compaction_keep(data, descs, res, idx)
+    got = orc.compaction_rewrite(data, descs, res, idx, keep)
+    seen = python_rewrite_check(data, descs, res, idx, keep, got)
+    assert {abi.COMPACT_FILTERED, abi.COMPACT_KEPT} <= seen
+    if fmt == DISK:
+        assert {abi.COMPACT_TX_CLEARED, abi.COMPACT_NOT_COMPACTIBLE} <= seen
+    # the compacted batches are valid batches whose records are the kept ones
+    ok = got["cres"]["out_len"] > 0
+    assert (got["out_results"]["verdict"][ok] == abi.V_OK).all()
+    assert (got["out_results"]["record_count"][ok] == got["cres"]["record_count"][ok]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", [DISK, WIRE])
+def test_gpu_compaction_rewrite(eng, fmt):
+    data, descs = rewrite_arena(7, nb=400, fmt=fmt)
+    res, idx, _ = orc.validate_arena(data, descs)
+    keep, _ = orc.compaction_keep(data, descs, res, idx)
+    want = orc.compaction_rewrite(data, descs, res, idx, keep)
+    got = eng.compaction_rewrite(data, descs, res, idx, keep)
+    for f in abi.COMPACT_RESULT_DTYPE.names:
+        bad = np.nonzero(got["cres"][f] != want["cres"][f])[0]
+        assert bad.size == 0, f"{f} differs at {bad[:8]}: gpu {got['cres'][f][bad[:8]]} oracle {want['cres'][f][bad[:8]]}"
+    assert got["out_bytes"] == want["out_bytes"]
+    assert np.array_equal(got["out"][:want["out_bytes"]], want["out"][:want["out_bytes"]])
+    for f in abi.RESULT_DTYPE.names:
+        assert np.array_equal(got["out_results"][f], want["out_results"][f]), f
+    assert got["used"] == want["used"]
+    assert np.array_equal(got["index"].view(np.uint8), want["index"].view(np.uint8))
