@@ -1,7 +1,7 @@
 // rpgpu_lz4c.h — LZ4 frame compression as lz4_frame_compressor::compress
 // produces it (compression/internal/lz4_frame_compressor.cc:68-158 over
 // liblz4 1.9.3), byte for byte: host + device code (the GPU's compress
-// lanes run it; tests/native/lz4c_fuzz.cpp compares it with liblz4 through
+// lanes run it; tests/native/compress_fuzz.cpp compares it with liblz4 through
 // the reference's loop).
 //
 // The reference's preferences (compression level 1, independent blocks,
