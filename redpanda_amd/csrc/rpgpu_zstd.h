@@ -256,17 +256,30 @@ RPC_HD bool huf_select_x2(uint64_t dst, uint64_t csrc) {
 }
 
 // ------------------------------------------------------------- workspace
-// Per-frame decoder state (per lane in HBM on the device; LDS for the scalar mirror): ~19 KB.
-struct Ws {
-    uint16_t huf[1u << kHufMaxLog];  // X1 table: symbol | nbBits << 8
+// Per-frame decoder state.  Two forms of one template:
+//   Ws  (kFull): the X1 Huffman table whole (4096 entries) -- per lane in HBM
+//        for the HBM lane decoder, LDS for the wave decoder and the scalar
+//        mirror: ~19 KB;
+//   WsC (compact, for workspaces in LDS one per lane): no X1 table; Huffman
+//        codes of up to kHuf1Log bits decode through huf1, longer ones from the
+//        code's weight band (hstart / hbase / hsym: the X1 table's layout
+//        without its copies, HUF_readDTableX1) -- ~7.6 KB.
+template <bool kFullHuf>
+struct WsT {
+    static constexpr bool kFull = kFullHuf;
+    uint16_t huf[kFullHuf ? (1u << kHufMaxLog) : 1];  // X1 table: symbol | nbBits << 8
     uint16_t huf1[1u << kHuf1Log];   // huf by the first kHuf1Log bits where that decides the code, else kHuf1None
     uint32_t ll[512], ml[512], of[256];  // sequence tables: state << 16 | nbBits << 8 | symbol
-    uint32_t llx[512], mlx[512];     // per state: baseline | extra bits << 24 (ZSTD_seqSymbol's
-                                     // baseValue / nbAdditionalBits: no dependent lookup per field)
+    uint32_t llx[kFullHuf ? 512 : 1], mlx[kFullHuf ? 512 : 1];  // per state: baseline | extra bits << 24
+                                     // (ZSTD_seqSymbol's baseValue / nbAdditionalBits: no dependent
+                                     // lookup per field; wave decoders only)
     uint32_t wt[64];                 // HUF weight FSE table: state << 16 | nbBits << 8 | symbol
     int16_t norm[256];
     uint16_t next[256];
     uint8_t w[256];                  // Huffman weights
+    uint8_t hsym[kFullHuf ? 1 : 256];  // WsC: symbols by (weight, symbol), the X1 table's order
+    uint16_t hstart[kHufMaxLog + 2];   // WsC: first X1 index of each weight
+    uint16_t hbase[kHufMaxLog + 2];    // WsC: first hsym index of each weight
     uint32_t rank[kHufMaxLog + 1];
     uint64_t rep[3];
     uint8_t ll_log, ml_log, of_log, huf_log;
@@ -275,6 +288,8 @@ struct Ws {
     uint64_t t_lit, t_seq, n_seq, n_lit;  // diagnostics build: clock64 per phase
 #endif
 };
+using Ws = WsT<true>;
+using WsC = WsT<false>;
 #if RPZ_PROF && defined(__HIP_DEVICE_COMPILE__)
 #define RPZ_CLK() ((uint64_t)clock64())
 #else
@@ -511,7 +526,8 @@ RPC_HD bool build_fse(uint32_t* t, uint16_t* next, const int16_t* norm, uint32_t
 // ---------------------------------------------------------------- Huffman
 // HUF_readStats (+ FSE_decompress_wksp for the weights, maxLog 6) and the X1
 // table (HUF_readDTableX1).  Returns header bytes or -1.
-RPC_HD int64_t huf_read_table(Ws& w, const uint8_t* in, uint64_t n) {
+template <class W>
+RPC_HD int64_t huf_read_table(W& w, const uint8_t* in, uint64_t n) {
     if (n == 0) return RPZ_FAIL(-1);
     uint64_t iSize = in[0], oSize;
     if (iSize >= 128) {
@@ -573,27 +589,57 @@ RPC_HD int64_t huf_read_table(Ws& w, const uint8_t* in, uint64_t n) {
     if (w.rank[1] < 2 || (w.rank[1] & 1)) return RPZ_FAIL(-1);
     const uint32_t nsym = (uint32_t)oSize + 1;
     // X1 table: ranks by weight ascending, symbols in order within a weight
-    uint32_t start = 0;
-    for (uint32_t r = 1; r <= log; r++) {
-        const uint32_t cur = start;
-        start += w.rank[r] << (r - 1);
-        w.rank[r] = cur;
-    }
-    for (uint32_t s = 0; s < nsym; s++) {
-        const uint32_t wt = w.w[s];
-        if (!wt) continue;
-        const uint32_t len = (1u << wt) >> 1;
-        const uint16_t d = (uint16_t)(s | ((log + 1 - wt) << 8));
-        for (uint32_t u = 0; u < len; u++) w.huf[w.rank[wt] + u] = d;
-        w.rank[wt] += len;
-    }
-    w.huf_log = (uint8_t)log;
-    w.huf1_on = log > kHuf1Log;
-    if (w.huf1_on)
-        for (uint32_t i = 0; i < (1u << kHuf1Log); i++) {
-            const uint16_t e = w.huf[i << (log - kHuf1Log)];
-            w.huf1[i] = (e >> 8) <= kHuf1Log ? e : kHuf1None;
+    if constexpr (W::kFull) {
+        uint32_t start = 0;
+        for (uint32_t r = 1; r <= log; r++) {
+            const uint32_t cur = start;
+            start += w.rank[r] << (r - 1);
+            w.rank[r] = cur;
         }
+        for (uint32_t s = 0; s < nsym; s++) {
+            const uint32_t wt = w.w[s];
+            if (!wt) continue;
+            const uint32_t len = (1u << wt) >> 1;
+            const uint16_t d = (uint16_t)(s | ((log + 1 - wt) << 8));
+            for (uint32_t u = 0; u < len; u++) w.huf[w.rank[wt] + u] = d;
+            w.rank[wt] += len;
+        }
+        w.huf_log = (uint8_t)log;
+        w.huf1_on = log > kHuf1Log;
+        if (w.huf1_on)
+            for (uint32_t i = 0; i < (1u << kHuf1Log); i++) {
+                const uint16_t e = w.huf[i << (log - kHuf1Log)];
+                w.huf1[i] = (e >> 8) <= kHuf1Log ? e : kHuf1None;
+            }
+    } else {
+        // the same layout without the copies: weight r's symbols occupy X1
+        // indexes [hstart[r], hstart[r + 1]), 2^(r-1) each, in symbol order
+        uint32_t start = 0, base = 0;
+        for (uint32_t r = 1; r <= log; r++) {
+            w.hstart[r] = (uint16_t)start;
+            w.hbase[r] = (uint16_t)base;
+            start += w.rank[r] << (r - 1);
+            base += w.rank[r];
+            w.rank[r] = w.hbase[r];
+        }
+        w.hstart[log + 1] = (uint16_t)start;
+        for (uint32_t s = 0; s < nsym; s++) {
+            const uint32_t wt = w.w[s];
+            if (wt) w.hsym[w.rank[wt]++] = (uint8_t)s;
+        }
+        w.huf_log = (uint8_t)log;
+        w.huf1_on = 1;
+        // huf1: the first min(log, kHuf1Log) bits; a code that fits decides
+        const uint32_t L1 = log < kHuf1Log ? log : kHuf1Log;
+        for (uint32_t i = 0; i < (1u << L1); i++) {
+            const uint32_t v = i << (log - L1);  // the X1 index of the first entry
+            uint32_t r = 1;
+            while (r < log && v >= w.hstart[r + 1]) r++;
+            const uint32_t nb = log + 1 - r;
+            w.huf1[i] = nb <= L1 ? (uint16_t)(w.hsym[w.hbase[r] + ((v - w.hstart[r]) >> (r - 1))] | (nb << 8))
+                                 : kHuf1None;
+        }
+    }
     return (int64_t)iSize + 1;
 }
 
@@ -633,14 +679,26 @@ RPC_HD void huf_end(HufS& h) {
     h.ok = h.ok && h.b.pos == 0;
 }
 // the X1 entry of the L-bit index v (two: through huf1 first)
-RPC_HD uint32_t huf_entry(const Ws& w, uint32_t v, uint32_t L, bool two) {
-    if (two) {
+template <class W>
+RPC_HD uint32_t huf_entry(const W& w, uint32_t v, uint32_t L, bool two) {
+    if constexpr (W::kFull) {
+        if (two) {
+            const uint32_t t = w.huf1[v >> (L - kHuf1Log)];
+            if (t != kHuf1None) return t;
+        }
+        return w.huf[v];
+    } else {
+        if (L <= kHuf1Log) return w.huf1[v];
         const uint32_t t = w.huf1[v >> (L - kHuf1Log)];
         if (t != kHuf1None) return t;
+        // a code longer than kHuf1Log bits: weight r < L + 1 - kHuf1Log
+        uint32_t r = 1;
+        while (r + kHuf1Log < L && v >= w.hstart[r + 1]) r++;
+        return (uint32_t)w.hsym[w.hbase[r] + ((v - w.hstart[r]) >> (r - 1))] | ((L + 1 - r) << 8);
     }
-    return w.huf[v];
 }
-RPC_HD void huf_step(const Ws& w, HufS& h, uint32_t L, bool x2, bool two = false) {
+template <class W>
+RPC_HD void huf_step(const W& w, HufS& h, uint32_t L, bool x2, bool two = false) {
     if (!h.live) return;
     if (h.b.pos < 0) {
         h.ok = false;
@@ -677,7 +735,8 @@ RPC_HD void huf_step(const Ws& w, HufS& h, uint32_t L, bool x2, bool two = false
     h.i = i + 1;
     if (h.i == h.nsym) huf_end(h);
 }
-RPC_HD bool huf_stream(const Ws& w, const uint8_t* src, uint64_t len, uint8_t* out, uint64_t nsym, uint64_t nwrite,
+template <class W>
+RPC_HD bool huf_stream(const W& w, const uint8_t* src, uint64_t len, uint8_t* out, uint64_t nsym, uint64_t nwrite,
                        bool two = false) {
     HufS h;
     if (!huf_begin(h, src, len, out, nsym, nwrite)) return RPZ_FAIL(false);
@@ -719,10 +778,12 @@ struct DirectEmit {
     // where a block's Huffman / RLE literals are decoded
     RPC_HD uint8_t* litbuf(uint8_t* out, uint64_t tail, uint64_t size) { return out + tail - size; }
     RPC_HD void litfill(uint8_t* d, uint8_t v, uint64_t n) { fill_bytes(d, v, n); }
-    RPC_HD bool huf1(const Ws& w, const uint8_t* src, uint64_t len, uint8_t* d, uint64_t n) {
+    template <class W>
+    RPC_HD bool huf1(const W& w, const uint8_t* src, uint64_t len, uint8_t* d, uint64_t n) {
         return huf_stream(w, src, len, d, n, n, w.huf1_on != 0);  // Ws in HBM: the first-level table
     }
-    RPC_HD bool huf4(const Ws& w, const Huf4& a) {
+    template <class W>
+    RPC_HD bool huf4(const W& w, const Huf4& a) {
         const uint32_t L = w.huf_log;
         const bool x2 = w.huf_x2 != 0;
         const bool two = w.huf1_on != 0;  // Ws in HBM: the first-level table
@@ -753,8 +814,8 @@ struct Lit {
 
 // ZSTD_decodeLiteralsBlock.  Huffman / RLE literals go to out[tail - n, tail).
 // Returns section bytes, -1 on error, -2 when the tail would reach `op`.
-template <class E>
-RPZ_COLD int64_t literals(E& em, Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t op, uint64_t tail,
+template <class E, class W>
+RPZ_COLD int64_t literals(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t op, uint64_t tail,
                           Lit& lit) {
     if (n < 3) return RPZ_FAIL(-1);  // MIN_CBLOCK_SIZE
     const uint32_t type = in[0] & 3, lh = (in[0] >> 2) & 3;
@@ -873,7 +934,9 @@ RPC_HD void build_default(uint32_t* t, uint16_t* next, int16_t* norm, const int8
 }
 
 // ZSTD_buildSeqTable for one of LL / OF / ML.  Returns bytes or -1.
-RPC_HD void seq_extra(Ws& w, uint32_t which) {
+template <class W>
+RPC_HD void seq_extra(W& w, uint32_t which) {
+    if constexpr (!W::kFull) return;
     if (which == 1) return;
     const uint32_t* t = which == 0 ? w.ll : w.ml;
     uint32_t* x = which == 0 ? w.llx : w.mlx;
@@ -883,17 +946,20 @@ RPC_HD void seq_extra(Ws& w, uint32_t which) {
         x[u] = which == 0 ? (kLLBase[c] | ((uint32_t)kLLBits[c] << 24)) : (kMLBase[c] | ((uint32_t)kMLBits[c] << 24));
     }
 }
-RPC_HD int64_t seq_table_impl(Ws& w, uint32_t mode, uint32_t which, const uint8_t* in, uint64_t n);
+template <class W>
+RPC_HD int64_t seq_table_impl(W& w, uint32_t mode, uint32_t which, const uint8_t* in, uint64_t n);
 // extra: also fill the per-state baseline tables (llx / mlx) -- for workspaces
 // in LDS, where they save a dependent lookup; a workspace in HBM reads the
 // baselines from the 89-entry code tables instead (one cached line, not a
 // line of HBM per sequence)
-RPC_HD int64_t seq_table(Ws& w, uint32_t mode, uint32_t which, const uint8_t* in, uint64_t n, bool extra) {
+template <class W>
+RPC_HD int64_t seq_table(W& w, uint32_t mode, uint32_t which, const uint8_t* in, uint64_t n, bool extra) {
     const int64_t h = seq_table_impl(w, mode, which, in, n);
     if (extra && h >= 0 && mode != 3) seq_extra(w, which);
     return h;
 }
-RPC_HD int64_t seq_table_impl(Ws& w, uint32_t mode, uint32_t which, const uint8_t* in, uint64_t n) {
+template <class W>
+RPC_HD int64_t seq_table_impl(W& w, uint32_t mode, uint32_t which, const uint8_t* in, uint64_t n) {
     uint32_t* t = which == 0 ? w.ll : (which == 1 ? w.of : w.ml);
     uint8_t& log = which == 0 ? w.ll_log : (which == 1 ? w.of_log : w.ml_log);
     const uint32_t max = which == 0 ? 35u : (which == 1 ? 31u : 52u);
@@ -928,11 +994,11 @@ RPC_HD int64_t seq_table_impl(Ws& w, uint32_t mode, uint32_t which, const uint8_
 // ZSTD_decompressBlock_internal for one compressed block: output at out[op..),
 // history from out[fstart..), at most `cap` bytes; literals may use the slot
 // tail [.., tail).  Returns bytes produced, -1 error, -2 slot exceeded.
-template <class E>
-RPZ_COLD int64_t block(E& em, Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t fstart, uint64_t op,
+template <class E, class W>
+RPZ_COLD int64_t block(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t fstart, uint64_t op,
                        uint64_t cap, uint64_t tail) {
     if (n >= kBlockMax) return RPZ_FAIL(-1);
-    constexpr bool kLdsWs = E::kInlineBlocks;  // the wave decoders keep Ws in LDS
+    constexpr bool kLdsWs = E::kInlineBlocks && W::kFull;  // the wave decoders keep Ws in LDS
     Lit lit;
 #if RPZ_PROF
     const uint64_t c0 = RPZ_CLK();
@@ -1058,14 +1124,14 @@ RPZ_COLD int64_t block(E& em, Ws& w, const uint8_t* in, uint64_t n, uint8_t* out
 // block() out of line for the lane decoders (DirectEmit: inlined at both call
 // sites the lane kernel outgrew the instruction cache), inline for the wave
 // emitter (its state stays in registers, its workspace accesses LDS ops).
-template <class E>
-__attribute__((noinline)) RPZ_HD_NOINL int64_t block_noinline(E& em, Ws& w, const uint8_t* in, uint64_t n,
+template <class E, class W>
+__attribute__((noinline)) RPZ_HD_NOINL int64_t block_noinline(E& em, W& w, const uint8_t* in, uint64_t n,
                                                               uint8_t* out, uint64_t fstart, uint64_t op,
                                                               uint64_t cap, uint64_t tail) {
     return block(em, w, in, n, out, fstart, op, cap, tail);
 }
-template <class E>
-RPC_HD int64_t block_call(E& em, Ws& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t fstart, uint64_t op,
+template <class E, class W>
+RPC_HD int64_t block_call(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t fstart, uint64_t op,
                           uint64_t cap, uint64_t tail) {
     if constexpr (E::kInlineBlocks)
         return block(em, w, in, n, out, fstart, op, cap, tail);
@@ -1215,9 +1281,9 @@ RPC_HD bool adapt(Bufs& s, uint64_t need_in, uint64_t need_out) {
 // One call of the wrapper over one buffer.  out[0, cap) is the output slot.
 // Returns a verdict; *out_len = bytes produced.  `cap` too small for what the
 // library would produce -> V_OVERFLOW.
-template <class E>
+template <class E, class W>
 RPC_HD int32_t uncompress_impl(E& em, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len,
-                               Ws& w) {
+                               W& w) {
     uint64_t T = 0, p = 0;
     uint64_t S = 0;  // fill of the 64 KiB staging buffer `out` (may sit full)
     Bufs bufs{0, 0, 0};
@@ -1296,11 +1362,11 @@ RPC_HD int32_t uncompress_impl(E& em, const uint8_t* in, uint64_t n, uint8_t* ou
             continue;
         }
         // streaming (ZSTD_decompressContinue through the ring buffer)
-        const uint64_t W = h.window < 1024 ? 1024 : h.window;
-        if (W > kMaxWindow) return RPZ_FAIL(V_ERROR);  // frameParameter_windowTooLarge
+        const uint64_t win = h.window < 1024 ? 1024 : h.window;
+        if (win > kMaxWindow) return RPZ_FAIL(V_ERROR);  // frameParameter_windowTooLarge
         {
             const uint64_t need_in = h.bsm < 4 ? 4 : h.bsm;
-            const uint64_t ring = W + (W < kBlockMax ? W : kBlockMax) + 64;
+            const uint64_t ring = win + (win < kBlockMax ? win : kBlockMax) + 64;
             const uint64_t need_out = h.fcs < ring ? h.fcs : ring;
             if (!adapt(bufs, need_in, need_out)) return RPZ_FAIL(V_ERROR);  // memory_allocation: runtime_error
         }
@@ -1457,8 +1523,8 @@ RPC_HD uint64_t bound(const uint8_t* in, uint64_t n) {
     return b;
 }
 
-template <class E>
-RPC_HD int32_t uncompress(E& em, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len, Ws& w) {
+template <class E, class W>
+RPC_HD int32_t uncompress(E& em, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len, W& w) {
     *out_len = 0;
     if (n == 0) return RPZ_FAIL(V_ERROR);  // "Asked to stream_zstd::uncompress empty buffer"
     const int32_t v = uncompress_impl(em, in, n, out, cap, out_len, w);
