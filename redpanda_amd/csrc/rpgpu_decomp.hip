@@ -61,7 +61,27 @@ constexpr uint64_t kLitScratch = (128u << 10) + 256;  // ZSTD_BLOCKSIZE_MAX + sl
 #define RPZ_LANES 131072  // 2 waves per SIMD at the lane kernel's VGPR count
 #endif
 constexpr uint32_t kZstdLanes = RPZ_LANES;
+union LaneWsZ {  // RPGPU_ZSTD_HBM: a zstd lane's workspace in HBM
+    rpzstd::Ws z;
+    rpinfl::Ws g;
+};
+// RPGPU_ZSTD_HBM=1: zstd through the HBM-workspace lane decoder (A/B
+// measurements of the LDS one); otherwise only gzip keeps lane workspaces in
+// HBM, 2 KB each for at most kGzipLanes lanes (gzip is in no benchmark
+// configuration)
+bool zstd_hbm() {
+    static const int v = [] {
+        const char* e = getenv("RPGPU_ZSTD_HBM");
+        return e && atoi(e) != 0 ? 1 : 0;
+    }();
+    return v != 0;
+}
+constexpr uint32_t kGzipLanes = 32768;
 uint32_t zstd_lanes(uint32_t n) { return n < kZstdLanes ? n : kZstdLanes; }
+uint32_t gzip_lanes(uint32_t n) { return n < kGzipLanes ? n : kGzipLanes; }
+size_t ws_region(uint32_t n) {
+    return zstd_hbm() ? (size_t)zstd_lanes(n) * sizeof(LaneWsZ) : (size_t)gzip_lanes(n) * sizeof(rpinfl::Ws);
+}
 // lanes in flight for the lane decoders (tuning knobs for measurements:
 // RPGPU_LZ_LANES, RPGPU_ZSTD_LANES; the scratch is sized for zstd_lanes(n))
 uint32_t env_lanes(const char* name, uint32_t dflt) {
@@ -72,10 +92,6 @@ uint32_t env_lanes(const char* name, uint32_t dflt) {
 uint32_t decomp_waves(uint32_t n) { return n < kDecompWaves ? n : kDecompWaves; }
 // scratch: slot[n] u64 | local[n] u64 | block_sum[nb] u64 | validate scratch |
 //          counters (256 B) | wave literal scratch[waves] | lane Ws[lanes]
-union LaneWs {
-    rpzstd::Ws z;
-    rpinfl::Ws g;
-};
 // one part of a split body (rpcodec::lz4f_split / snappy_java_split)
 struct SplitPart {
     uint32_t batch, kind, in_off, in_len;  // offsets within the batch body
@@ -93,7 +109,8 @@ struct Parts {
     void* vscratch;
     uint32_t* counter;
     uint8_t* lits;
-    LaneWs* zws;
+    LaneWsZ* zws;     // zstd lanes (RPGPU_ZSTD_HBM) ...
+    rpinfl::Ws* gws;  // ... or gzip lanes: the same region
 };
 size_t parts_head(uint32_t n) {
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
@@ -102,7 +119,7 @@ size_t parts_head(uint32_t n) {
 size_t counter_offset(uint32_t n) { return (parts_head(n) + validate_scratch_bytes(n) + 255) & ~(size_t)255; }
 size_t zws_offset(uint32_t n) { return counter_offset(n) + 256 + (size_t)decomp_waves(n) * kLitScratch; }
 size_t parts_offset(uint32_t n) {
-    return (zws_offset(n) + (size_t)zstd_lanes(n) * sizeof(LaneWs) + 255) & ~(size_t)255;
+    return (zws_offset(n) + ws_region(n) + 255) & ~(size_t)255;
 }
 Parts parts(void* p, uint32_t n) {
     uint8_t* b = static_cast<uint8_t*>(p);
@@ -116,7 +133,8 @@ Parts parts(void* p, uint32_t n) {
     s.vscratch = b + parts_head(n);
     s.counter = reinterpret_cast<uint32_t*>(b + counter_offset(n));
     s.lits = b + counter_offset(n) + 256;
-    s.zws = reinterpret_cast<LaneWs*>(b + zws_offset(n));
+    s.zws = reinterpret_cast<LaneWsZ*>(b + zws_offset(n));
+    s.gws = reinterpret_cast<rpinfl::Ws*>(b + zws_offset(n));
     s.parts = reinterpret_cast<SplitPart*>(b + parts_offset(n));
     s.pres = reinterpret_cast<int32_t*>(s.parts + part_cap(n));
     return s;
@@ -154,11 +172,11 @@ __device__ __forceinline__ uint64_t body_len(const rpgpu_batch_result& v) {
 __global__ __launch_bounds__(256) void gzip_bound_kernel(const rpgpu_batch_desc* __restrict__ descs, uint32_t n,
                                                          const uint8_t* __restrict__ data,
                                                          const rpgpu_batch_result* __restrict__ vres,
-                                                         uint64_t* __restrict__ slot, LaneWs* __restrict__ wsbuf) {
+                                                         uint64_t* __restrict__ slot, rpinfl::Ws* __restrict__ wsbuf) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lanes = gridDim.x * blockDim.x;
     if (g >= n) return;
-    rpinfl::Ws& ws = wsbuf[g].g;
+    rpinfl::Ws& ws = wsbuf[g];
     for (uint32_t i = g; i < n; i += lanes) {
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
@@ -414,11 +432,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_WS_WA
     const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
     rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
-    rpgpu_batch_desc* __restrict__ out_descs, LaneWs* __restrict__ wsbuf) {
+    rpgpu_batch_desc* __restrict__ out_descs, void* __restrict__ wsraw) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lanes = gridDim.x * blockDim.x;
     if (g >= n) return;  // lanes past the arena own no workspace
-    LaneWs& ws = wsbuf[g];
+    // gzip: 2 KB workspaces; zstd (RPGPU_ZSTD_HBM): the union
+    LaneWsZ& zws = reinterpret_cast<LaneWsZ*>(wsraw)[g];
+    rpinfl::Ws& gws = reinterpret_cast<rpinfl::Ws*>(wsraw)[g];
     for (uint32_t i = g; i < n; i += lanes) {
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
@@ -433,10 +453,50 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_WS_WA
             const uint64_t cap = sz - kHeaderSize - rpcodec::kSlack;
             if (FAM == 4) {
                 rpzstd::DirectEmit em;
-                verdict = rpzstd::uncompress(em, in, body_len(v), o, cap, &len, ws.z);
+                verdict = rpzstd::uncompress(em, in, body_len(v), o, cap, &len, zws.z);
             } else {
-                verdict = rpinfl::uncompress(in, body_len(v), o, cap, &len, ws.g);
+                verdict = rpinfl::uncompress(in, body_len(v), o, cap, &len, gws);
             }
+        }
+        finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
+    }
+}
+
+// zstd batches up to kZstdLaneMaxSlot: one lane per batch with its workspace in
+// LDS -- the compact form (rpzstd::WsC, ~7.6 KB: sequence FSE tables, the
+// first-level Huffman table and weight bands), so every table lookup of the
+// entropy decoders is an LDS access instead of a line of HBM (the HBM lane
+// workspaces cost ~35x the algorithmic bytes in traffic).  A
+// workgroup is one wave of which ZL lanes decode (the LDS holds ZL
+// workspaces); lanes stride over the arena's batches.
+#ifndef RPZ_LDS_LANES
+#define RPZ_LDS_LANES 5
+#endif
+constexpr uint32_t kZLdsLanes = RPZ_LDS_LANES;
+template <uint32_t ZL>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void zstd_lds_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
+    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
+    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
+    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
+    rpgpu_batch_desc* __restrict__ out_descs) {
+    __shared__ rpzstd::WsC wsl[ZL];
+    const uint32_t lid = threadIdx.x;
+    if (lid >= ZL) return;
+    rpzstd::WsC& ws = wsl[lid];
+    const uint32_t lanes = gridDim.x * ZL;
+    for (uint32_t i = blockIdx.x * ZL + lid; i < n; i += lanes) {
+        const rpgpu_batch_desc d = descs[i];
+        const rpgpu_batch_result v = vres[i];
+        uint64_t sz = slot[i];
+        if (!decomp_wanted(d, v) || v.codec != 4 || wave_owned(d, v, sz)) continue;
+        const uint64_t off = block_base[i / kScanBlock] + local[i];
+        int32_t verdict = RPGPU_V_SKIPPED;
+        uint64_t len = 0;
+        if (plan_slot(sz, off, out_cap, verdict, len)) {
+            rpzstd::DirectEmit em;
+            verdict = rpzstd::uncompress(em, data + d.offset + kHeaderSize, body_len(v), out + off + kHeaderSize,
+                                         sz - kHeaderSize - rpcodec::kSlack, &len, ws);
         }
         finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
     }
@@ -623,8 +683,8 @@ hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const
     if (n == 0) return d_out_bytes ? hipMemsetAsync(d_out_bytes, 0, sizeof(uint64_t), s) : hipSuccess;
     const Parts p = parts(d_scratch, n);
     const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
-    const uint32_t zl = zstd_lanes(n);
-    gzip_bound_kernel<<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.zws);
+    const uint32_t gl = gzip_lanes(n);
+    gzip_bound_kernel<<<(gl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.gws);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // wave-owned batch lists (filled by decomp_caps_kernel): counters 2 and 3
@@ -695,11 +755,26 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     if ((e = hipGetLastError()) != hipSuccess) return e;
     static const uint32_t zs_lanes = env_lanes("RPGPU_ZSTD_LANES", kZstdLanes);
     const uint32_t zl = n < zs_lanes ? n : zs_lanes;
-    ws_lane_kernel<4><<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
-                                                         d_dres, d_out, out_cap, d_out_descs, p.zws);
+    if (zstd_hbm()) {  // the HBM-workspace lane decoder (A/B measurements)
+        ws_lane_kernel<4><<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
+                                                             d_dres, d_out, out_cap, d_out_descs, p.zws);
+    } else {
+        static int zgrid = 0;
+        if (!zgrid) {
+            int dev = 0, cus = 0, per = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, zstd_lds_kernel<kZLdsLanes>, 64, 0);
+            zgrid = (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
+        }
+        const uint32_t need = (n + kZLdsLanes - 1) / kZLdsLanes;
+        zstd_lds_kernel<kZLdsLanes><<<(uint32_t)zgrid < need ? (uint32_t)zgrid : need, 64, 0, s>>>(
+            d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    ws_lane_kernel<1><<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
-                                                         d_dres, d_out, out_cap, d_out_descs, p.zws);
+    const uint32_t gl = gzip_lanes(n);
+    ws_lane_kernel<1><<<(gl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
+                                                         d_dres, d_out, out_cap, d_out_descs, p.gws);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ds) {
         if ((e = hipEventRecord(ds->join, ds->aux)) != hipSuccess) return e;
