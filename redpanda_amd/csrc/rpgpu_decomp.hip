@@ -153,6 +153,13 @@ constexpr uint64_t kLaneMaxSlot = 256u << 10;
 #endif
 constexpr uint64_t kZstdLaneMaxSlot = RPGPU_ZSTD_LANE_MAX;  // zstd: its lane / wave boundary
 __device__ __forceinline__ uint64_t lane_max(uint32_t codec) { return codec == 4 ? kZstdLaneMaxSlot : kLaneMaxSlot; }
+// LZ4 / snappy-java slots above this are split into parts when the frame allows
+// (at most kLaneMaxSlot: the lane decoders take the unsplit ones below it)
+#ifndef RPGPU_SPLIT_MIN
+#define RPGPU_SPLIT_MIN (256u << 10)
+#endif
+constexpr uint64_t kSplitMinSlot = RPGPU_SPLIT_MIN;
+static_assert(kSplitMinSlot <= kLaneMaxSlot, "split threshold above the lane decoders' limit");
 
 // slot[i] of a batch whose bound exceeds the per-batch ceiling: kOverCeiling |
 // bound -- no output reserved (the scan counts 0), verdict DECOMP_OVERFLOW
@@ -234,7 +241,7 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
         // parts[pcap / 2..)); the rest to the wave decoders (zstd list at
         // wlist[0..), LZ list at wlist[n..))
         uint32_t sf = 0, sc = 0;
-        if (!over && sz > lane_max(vres[i].codec) && decomp_wanted(descs[i], vres[i])) {
+        if (!over && sz > (vres[i].codec == 4 ? lane_max(4) : kSplitMinSlot) && decomp_wanted(descs[i], vres[i])) {
             const uint32_t c = vres[i].codec;
             if (c == 2 || c == 3) {
                 const uint8_t* b = data + descs[i].offset + kHeaderSize;
@@ -273,7 +280,7 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
                     }
                 }
             }
-            if (!sc) {
+            if (!sc && sz > lane_max(c)) {
                 if (c == 4) wlist[atomicAdd(wcount, 1u)] = i;
                 else if (c == 2 || c == 3) wlist[n + atomicAdd(wcount + 1, 1u)] = i;
             }
@@ -392,7 +399,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_
     const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
     rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
-    rpgpu_batch_desc* __restrict__ out_descs) {
+    rpgpu_batch_desc* __restrict__ out_descs, const uint32_t* __restrict__ scount) {
     const uint32_t lanes = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += lanes) {
         uint64_t sz = slot[i], off = 0;
@@ -403,7 +410,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_
             const rpgpu_batch_result v = vres[i];
             const bool want = decomp_wanted(d, v);
             // this instance's batches: its codec's lane-sized ones (+ for LZ4, the undecoded)
-            const bool mine = want ? (v.codec == CODEC && !wave_owned(d, v, sz)) : CODEC == 3;
+            const bool mine = want ? (v.codec == CODEC && !wave_owned(d, v, sz) && scount[i] == 0) : CODEC == 3;
             if (!mine) continue;
             off = block_base[i / kScanBlock] + local[i];
             if (want && plan_slot(sz, off, out_cap, verdict, len)) {
@@ -728,7 +735,24 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     if (ds) {
         if ((e = hipEventRecord(ds->parts, s)) != hipSuccess) return e;
     }
-    // the zstd wave decoder first on the second stream: it does not wait for the parts
+    // zstd first on the second stream: the LDS lane decoder (its workgroups
+    // hold the LDS; the LZ4 / snappy lane kernels on the main stream hold
+    // registers, so both fit the CUs at once), then the wave decoder for frames
+    // above kZstdLaneMaxSlot; neither waits for the parts
+    if (!zstd_hbm()) {
+        static int zgrid = 0;
+        if (!zgrid) {
+            int dev = 0, cus = 0, per = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, zstd_lds_kernel<kZLdsLanes>, 64, 0);
+            zgrid = (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
+        }
+        const uint32_t need = (n + kZLdsLanes - 1) / kZLdsLanes;
+        zstd_lds_kernel<kZLdsLanes><<<(uint32_t)zgrid < need ? (uint32_t)zgrid : need, 64, 0, ws>>>(
+            d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     decomp_wave_kernel<kFamZstd><<<decomp_waves(n), 64, sizeof(rpzstd::Ws), ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
                                                                 p.block_sum, d_dres, d_out, out_cap, d_out_descs,
                                                                 p.counter + 1, p.lits, p.wlist, p.counter + 2);
@@ -749,29 +773,17 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     const uint32_t lzl = n < lz_lanes ? n : lz_lanes;
     const uint32_t lzb = (lzl + 255) / 256;
     decomp_lane_kernel<3><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
-                                              out_cap, d_out_descs);
+                                              out_cap, d_out_descs, p.scount);
     decomp_lane_kernel<2><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
-                                              out_cap, d_out_descs);
+                                              out_cap, d_out_descs, p.scount);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    static const uint32_t zs_lanes = env_lanes("RPGPU_ZSTD_LANES", kZstdLanes);
-    const uint32_t zl = n < zs_lanes ? n : zs_lanes;
     if (zstd_hbm()) {  // the HBM-workspace lane decoder (A/B measurements)
+        static const uint32_t zs_lanes = env_lanes("RPGPU_ZSTD_LANES", kZstdLanes);
+        const uint32_t zl = n < zs_lanes ? n : zs_lanes;
         ws_lane_kernel<4><<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
                                                              d_dres, d_out, out_cap, d_out_descs, p.zws);
-    } else {
-        static int zgrid = 0;
-        if (!zgrid) {
-            int dev = 0, cus = 0, per = 0;
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, zstd_lds_kernel<kZLdsLanes>, 64, 0);
-            zgrid = (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
-        }
-        const uint32_t need = (n + kZLdsLanes - 1) / kZLdsLanes;
-        zstd_lds_kernel<kZLdsLanes><<<(uint32_t)zgrid < need ? (uint32_t)zgrid : need, 64, 0, s>>>(
-            d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t gl = gzip_lanes(n);
     ws_lane_kernel<1><<<(gl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
                                                          d_dres, d_out, out_cap, d_out_descs, p.gws);
