@@ -65,14 +65,16 @@ union LaneWsZ {  // RPGPU_ZSTD_HBM: a zstd lane's workspace in HBM
     rpzstd::Ws z;
     rpinfl::Ws g;
 };
-// RPGPU_ZSTD_HBM=1: zstd through the HBM-workspace lane decoder (A/B
-// measurements of the LDS one); otherwise only gzip keeps lane workspaces in
-// HBM, 2 KB each for at most kGzipLanes lanes (gzip is in no benchmark
-// configuration)
+// zstd lanes keep their workspaces in HBM (the default) or, with
+// RPGPU_ZSTD_LDS=1, in LDS (zstd_lds_kernel: measured 3.25 s vs 0.585 s per C4
+// step -- the lane's chain of dependent global accesses per sequence, not its
+// table lookups, sets a lane's pace, and the LDS holds 20 lanes per CU against
+// 512 in HBM); gzip lanes keep theirs in HBM, 2 KB each for at most kGzipLanes
+// lanes (gzip is in no benchmark configuration)
 bool zstd_hbm() {
     static const int v = [] {
-        const char* e = getenv("RPGPU_ZSTD_HBM");
-        return e && atoi(e) != 0 ? 1 : 0;
+        const char* e = getenv("RPGPU_ZSTD_LDS");
+        return e && atoi(e) != 0 ? 0 : 1;
     }();
     return v != 0;
 }
@@ -777,7 +779,7 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     decomp_lane_kernel<2><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
                                               out_cap, d_out_descs, p.scount);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (zstd_hbm()) {  // the HBM-workspace lane decoder (A/B measurements)
+    if (zstd_hbm()) {  // the HBM-workspace lane decoder
         static const uint32_t zs_lanes = env_lanes("RPGPU_ZSTD_LANES", kZstdLanes);
         const uint32_t zl = n < zs_lanes ? n : zs_lanes;
         ws_lane_kernel<4><<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
