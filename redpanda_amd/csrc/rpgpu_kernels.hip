@@ -176,9 +176,12 @@ typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t batch_rsrc(const uint8_t* p) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p), 0, 0x7ffffff0, 0x00020000);
 }
+#ifndef RPGPU_ROW_AUX
+#define RPGPU_ROW_AUX 2  // row loads non-temporal (nt): C2 4.44 -> 4.18 ms per launch vs the default policy
+#endif
 __device__ __forceinline__ u32x4 load_row(__amdgpu_buffer_rsrc_t rs, const Geom& gm, int32_t row, uint32_t l) {
     const int32_t rb = row < gm.niter ? gm.g0 + (row << 10) : (int32_t)0x80000000;
-    const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, rb + (int32_t)(16 * l), 0, 0);
+    const i32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, rb + (int32_t)(16 * l), 0, RPGPU_ROW_AUX);
     return (u32x4){(uint32_t)v.x, (uint32_t)v.y, (uint32_t)v.z, (uint32_t)v.w};
 }
 
