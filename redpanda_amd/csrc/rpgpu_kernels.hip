@@ -232,8 +232,7 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
                                               uint32_t b, const uint8_t* __restrict__ data,
                                               rpgpu_batch_result* __restrict__ res, uint32_t index_first,
                                               Prefetch& pf, const rpgpu_batch_desc& nd,
-                                              bool has_next, uint32_t* __restrict__ ring, uint32_t slice_cap,
-                                              rpgpu_record_index* __restrict__ index DIAG_PARAM) {
+                                              bool has_next DIAG_PARAM) {
     const uint32_t l = lane_id();
     const uint8_t* p = data + d.offset;
     const uint32_t len = d.length;
@@ -400,22 +399,6 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
     const __amdgpu_buffer_rsrc_t rs = batch_rsrc(p);
     const __amdgpu_buffer_rsrc_t nrs_rows = batch_rsrc(data + (has_next ? nd.offset : 0));
     uint32_t c = 0;
-#ifdef RPGPU_FUSED_WALK
-    // the record walk rides on the rows (rpgpu_walk.h rw_row), speculatively:
-    // its verdict and entries count only if the CRC matches
-    const bool walk = (d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX)) && (r.h.attrs & 7) == 0 && !body_trunc;
-    const bool want_index = (d.ops & RPGPU_OP_INDEX) != 0;
-    rw::State W;
-    rw::init(W, walk, (int32_t)n, r.h.record_count, slice_cap);
-    rpgpu_record_index* const idx = index + index_first;
-    RingCand cand;
-    cand.ring = ring;
-    cand.cur = 16;  // slot 0's byte address: the pair's first row
-    cand.n = (int32_t)n;
-    cand.base_offset = r.h.base_offset;
-    cand.first_ts = r.h.first_ts;
-    cand.idx = idx;
-#endif
     STAMP(0);
     if (!pf_ok) load_rows(pf.x, rs, gm, 0, l);
     // the header bytes lie in rows 0 and 1
@@ -433,26 +416,6 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
 #pragma unroll
         for (int k = 0; k < kRowsPerChunk; k++) {
             u32x4 y = pf.x[k];
-#ifdef RPGPU_FUSED_WALK
-            // rows go to the ring in pairs (row 2m in slot 0, 2m + 1 in slot 1,
-            // whose last 16 bytes also go in front of slot 0 for the pair
-            // after); the walk takes each pair once both are there
-            if (W.kind != rw::kFDone) {
-                const int slot = 4 + 256 * (k & 1);
-                *reinterpret_cast<u32x4*>(ring + slot + 4 * l) = y;
-                if (k & 1) {
-                    const int32_t P0 = gm.g0 + ((cb + k - 1) << 10);  // the pair's first row
-                    if (cb + k - 1 < gm.niter && kHeaderSize + W.wp < P0 + 2048) {
-                        wave_lds_sync();
-                        cand.R0 = P0;
-                        const int32_t pend = P0 + 2048;
-                        rw::run(W, cand, pend < (int32_t)n ? pend : (int32_t)n, pend >= (int32_t)n, want_index);
-                        wave_lds_sync();
-                    }
-                    if (l == 63) *reinterpret_cast<u32x4*>(ring) = y;
-                }
-            }
-#endif
             y.x ^= c;
             c = crc_block(sN, y);
             pf.x[k] = load_row(lrs, lg, lrow + k, l);
@@ -488,20 +451,6 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
     } else if (codec > 4) {
         r.verdict = RPGPU_V_BAD_CODEC_THROW;
     }
-#ifdef RPGPU_FUSED_WALK
-    if (walk) {
-        const uint32_t m = want_index ? (W.cnt < slice_cap ? W.cnt : slice_cap) : 0u;
-        if (r.verdict == RPGPU_V_OK) {
-            r.verdict = W.verdict;
-            r.index_count = m;
-        } else {
-            // the CRC failed: no walk happened (kafka_batch_adapter.cc:169-193);
-            // undo the entries stored on the way
-            for (uint32_t e = l; e < 2 * m; e += 64)
-                reinterpret_cast<u32x4*>(idx)[e] = (u32x4){0u, 0u, 0u, 0u};
-        }
-    }
-#endif
     write_result(res + b, r);
     STAMP(3);
 }
@@ -515,18 +464,10 @@ __global__ __launch_bounds__(kValidateThreads) void validate_kernel(
     const uint32_t* __restrict__ local_first, const uint32_t* __restrict__ caps,
     const uint64_t* __restrict__ block_base, uint64_t index_cap, const uint32_t* __restrict__ tables) {
     __shared__ __attribute__((aligned(16))) uint32_t sT[kTableWords];
-#ifdef RPGPU_FUSED_WALK
-    __shared__ __attribute__((aligned(16))) uint32_t s_ring[kWavesPerBlock][kRingDwords];
-#endif
     load_tables(sT, tables);
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + wave);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
-#ifdef RPGPU_FUSED_WALK
-    uint32_t* const ring = s_ring[wave];
-#else
-    uint32_t* const ring = nullptr;
-#endif
 #ifdef RPGPU_DIAG_STAMPS
     Stamps sp{};
     sp.prev = __builtin_amdgcn_s_memtime();
@@ -549,14 +490,7 @@ __global__ __launch_bounds__(kValidateThreads) void validate_kernel(
         // is lowered to scratch memory
         const rpgpu_batch_desc nd = sload_desc(descs + (has_next ? b + nw : b));
         const uint64_t first = sload(block_base + b / kScanBlock) + sload(local_first + b);
-        uint32_t slice = 0;  // the batch's index slice, clamped to the caller's buffer
-#ifdef RPGPU_FUSED_WALK
-        {
-            const uint64_t cap = sload(caps + b);
-            slice = first >= index_cap ? 0u : (uint32_t)(first + cap > index_cap ? index_cap - first : cap);
-        }
-#endif
-        process_batch(sT, d, b, data, res, (uint32_t)first, pf, nd, has_next, ring, slice, index DIAG_PASS);
+        process_batch(sT, d, b, data, res, (uint32_t)first, pf, nd, has_next DIAG_PASS);
         STAMP(5);
     }
 #ifdef RPGPU_DIAG_STAMPS
@@ -1185,12 +1119,7 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
     uint32_t *caps, *local_first;
     uint64_t* block_sum;
     scratch_parts(const_cast<void*>(d_scratch), n, &caps, &local_first, &block_sum);
-#ifdef RPGPU_FUSED_WALK
-    const uint32_t chunks = 1;  // the walk is in validate_kernel: nothing to overlap
-    (void)ov;
-#else
     const uint32_t chunks = (ov && n >= kRunChunkMin) ? (uint32_t)ov->chunks : 1u;
-#endif
     hipError_t e = hipSuccess;
     for (uint32_t k = 0; k < chunks; k++) {
         const uint32_t lo = (uint32_t)((uint64_t)n * k / chunks), hi = (uint32_t)((uint64_t)n * (k + 1) / chunks);
@@ -1205,11 +1134,9 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
             if ((e = hipStreamWaitEvent(ov->aux, ov->ev[k], 0)) != hipSuccess) return e;
             ws = ov->aux;
         }
-#ifndef RPGPU_FUSED_WALK
         walk_kernel<<<(hi - lo + 255) / 256, 256, 0, ws>>>(d_descs, lo, hi, d_data, d_res, d_index, local_first,
                                                            caps, block_sum, index_cap);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-#endif
     }
     if (chunks > 1) {  // the caller's stream sees the last walk
         if ((e = hipEventRecord(ov->ev[chunks], ov->aux)) != hipSuccess) return e;

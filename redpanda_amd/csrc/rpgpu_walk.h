@@ -19,7 +19,6 @@
 #define RPGPU_WALK_H
 
 #include "rpgpu_device.h"
-#include "rpgpu_rowwalk.h"
 
 namespace rpgpu {
 
@@ -218,54 +217,6 @@ __device__ __forceinline__ void walk_lanes(const uint8_t* __restrict__ data, Wal
         r[15] = (J.flags & kJobIndex) ? (cnt < J.cap ? cnt : J.cap) : 0u;  // .index_count
     }
 }
-
-// ------------------------------------------------------------ fused row walk
-// RPGPU_FUSED_WALK: the walk's state machine (rpgpu_rowwalk.h) driven by
-// validate_kernel's wave over the rows it checksums.  The device candidate
-// provider: the row pair sits in a per-wave LDS ring (two 1 KiB slots behind a
-// 16-byte copy of the previous pair's tail, so the bytes before the pair are
-// contiguous with it); lane j decodes the varint that would start at q + j,
-// and the state machine reads candidates with readlanes.
-constexpr int kRingDwords = 4 + 256 + 256 + 24;  // tail | slot 0 | slot 1 | pad (window reads past the pair)
-static_assert(rw::kCopyLimit == kCopyLimit && rw::kHcountLimit == kHcountLimit, "walk limits");
-
-struct RingCand {
-    const uint32_t* ring;
-    int32_t cur, R0, n;
-    uint32_t vlo, vhi, nbv;
-    int64_t base_offset, first_ts;
-    rpgpu_record_index* idx;
-    __device__ __forceinline__ void decode(int32_t q) {
-        const int32_t x = q + (int32_t)lane_id();
-        const int32_t a = cur + (x - R0);  // byte address in the ring
-        const int32_t aw = a >> 2;
-        const uint32_t s = (uint32_t)a & 3u;
-        const uint32_t w0 = ring[aw], w1 = ring[aw + 1], w2 = ring[aw + 2], w3 = ring[aw + 3];
-        const uint32_t d0 = __builtin_amdgcn_alignbyte(w1, w0, s);
-        const uint32_t d1 = __builtin_amdgcn_alignbyte(w2, w1, s);
-        const uint32_t d2 = __builtin_amdgcn_alignbyte(w3, w2, s);
-        const int32_t left = n - x;
-        const uint32_t lim = left <= 0 ? 0u : (left < 10 ? (uint32_t)left : 10u);
-        uint64_t v;
-        nbv = rw::varint12(d0, d1, d2, lim, v);
-        vlo = (uint32_t)v;
-        vhi = (uint32_t)(v >> 32);
-    }
-    __device__ __forceinline__ uint32_t nb(uint32_t j) const {
-        return (uint32_t)__builtin_amdgcn_readlane((int)nbv, (int)j);
-    }
-    __device__ __forceinline__ int64_t val(uint32_t j) const {
-        return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)vhi, (int)j) << 32) |
-                         (uint32_t)__builtin_amdgcn_readlane((int)vlo, (int)j));
-    }
-    __device__ __forceinline__ void entry(uint32_t k, int32_t off, int64_t ts, int32_t koff, int64_t klen,
-                                          int32_t voff, int64_t vlen) {
-        if (lane_id() == 0)
-            store_entry(idx + k, (int64_t)((uint64_t)base_offset + (uint64_t)(int64_t)off),
-                        (int64_t)((uint64_t)first_ts + (uint64_t)ts), (uint32_t)(koff + kHeaderSize), (int32_t)klen,
-                        (uint32_t)(voff + kHeaderSize), (int32_t)vlen);
-    }
-};
 
 }  // namespace rpgpu
 #endif

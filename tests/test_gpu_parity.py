@@ -73,17 +73,26 @@ def test_crc32c_scalar_mirror(eng):
         assert eng.crc32c_extend(seed, b) == orc.crc32c(b, seed), n
 
 
-@pytest.mark.parametrize("case", ["headers", "ragged"])
+@pytest.mark.parametrize("case", ["headers", "ragged", "corrupt"])
 def test_walk_overlap_arenas(case):
-    """RPGPU_OPT_WALK_OVERLAP: an arena above kRunChunkMin (16384 batches) is
-    checksummed in chunks with each chunk's walk on a second stream; results
-    and index as the oracle's (uniform small batches, and ragged ones whose
-    walks differ in length)."""
-    kw = dict(CASES[case])
+    """RPGPU_OPT_WALK_OVERLAP on an arena above kRunChunkMin (16384 batches):
+    chunked checksums with each chunk's walk on a second stream.  Results and
+    index as the oracle's (uniform small batches, ragged ones whose walks
+    differ in length, and corrupted ones the walk must leave alone), on two
+    launches in a row."""
+    if case == "corrupt":
+        kw = dict(CASES["headers"], corrupt_ppm=50_000, corrupt_mask=0x1FF)
+    else:
+        kw = dict(CASES[case])
     if case == "ragged":
         kw["body_max"] = 3000
     spec = engine.make_spec(seed=zlib.crc32(case.encode()) + 7, format=abi.FMT_KAFKA_WIRE, **kw)
     data, descs = engine.build_arena(spec, 20000)
     with engine.Engine(0, walk_overlap=True) as e:
         got = e.submit(data, descs)
-    assert_same(*got, *orc.validate_arena(data, descs))
+        again = e.submit(data, descs)
+    want = orc.validate_arena(data, descs)
+    assert_same(*got, *want)
+    assert_same(*again, *want)
+    if case == "corrupt":
+        assert len(np.unique(want[0]["verdict"])) >= 4
