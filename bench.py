@@ -68,6 +68,7 @@ CONFIGS = {
                  "LZ4F decompression, batch rewrite with fresh CRCs, record walk + index of the "
                  "decompressed records",
         batches=1 << 18, partitions=4096, decompress=True, cpu_sample=2048,
+        ws_lanes=256,  # an LZ4 reader: the minimum of zstd / gzip workspaces (rpgpu_opts.decomp_ws_lanes)
         spec=dict(records_per_batch=64, key_len=16, value_len=999, codec=3)),
     "c4": dict(
         workload="C4: zstd-compressed Kafka v2 batches (the reference's compressor: level 3, pledged "
@@ -279,7 +280,7 @@ def main() -> int:
     if args.ops:
         spec.ops = args.ops
     # chunked checksum / walk overlap for the uniform uncompressed arenas (RPGPU_OPT_WALK_OVERLAP)
-    eng = engine.Engine(local, walk_overlap=not decompress)
+    eng = engine.Engine(local, walk_overlap=not decompress, decomp_ws_lanes=cfg.get("ws_lanes", 0))
     chunks, P_total, part_shift, (plo, phi) = rank_chunks(cfg, rank, world, scaling, args.batches)
     n = sum(m for _, m in chunks)
 
@@ -338,7 +339,7 @@ def main() -> int:
         # frames' block headers, so the buffers are sized once)
         eng.run_device(d_descs.data_ptr(), n, data.data_ptr(), d_res.data_ptr(),
                        d_index.data_ptr(), index_cap, d_scratch.data_ptr(), sh)
-        d_dscr = torch.zeros(engine.Engine.decomp_scratch_bytes(n), dtype=torch.uint8, device=dev)
+        d_dscr = torch.zeros(eng.decomp_scratch_bytes(n), dtype=torch.uint8, device=dev)
         d_obytes = torch.zeros(2, dtype=torch.int64, device=dev)
         eng.decomp_plan_device(d_descs.data_ptr(), n, data.data_ptr(), d_res.data_ptr(),
                                d_obytes.data_ptr(), d_dscr.data_ptr(), sh)

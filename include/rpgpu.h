@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RPGPU_ABI_VERSION 2
+#define RPGPU_ABI_VERSION 3
 #define RPGPU_ARENA_TAIL_PAD 64
 #define RPGPU_HEADER_SIZE 61 /* model/record.h:527-540 */
 
@@ -205,6 +205,14 @@ typedef struct rpgpu_opts {
      * output plan.  0 = RPGPU_DEFAULT_MAX_DECODED_BATCH.  Not a reference
      * limit: there the outcome depends on the broker's free memory. */
     uint64_t max_decoded_batch;
+    /* decompression: ceiling on the zstd / gzip decoder lanes, each with a
+     * ~20 KB workspace in the scratch (rpgpu_decomp_scratch_bytes_ctx).
+     * 0 = 131072 zstd / 32768 gzip lanes (2.6 GB for arenas of >= 131072
+     * batches: the C4 tuning); a reader whose arenas carry few or no zstd /
+     * gzip batches (an LZ4 or snappy topic) sets a small value (minimum 256):
+     * its zstd / gzip batches still decode, each lane taking more of them. */
+    uint32_t decomp_ws_lanes;
+    uint32_t reserved;     /* 0 */
 } rpgpu_opts;
 #define RPGPU_DEFAULT_MAX_DECODED_BATCH (64ull << 20)
 
@@ -352,9 +360,14 @@ typedef struct rpgpu_decomp_result {
 
 /* Scratch of the decompress path: the plan's slots and scans, the validation
  * scratch of the rewritten batches, one ~20 KB zstd workspace per decoder
- * lane (min(n, 131072) lanes: up to 2.6 GB, sized for HBM, not for the host)
+ * lane (min(n, 131072) lanes: up to 2.6 GB, sized for HBM, not for the host;
+ * fewer with rpgpu_opts.decomp_ws_lanes, see rpgpu_decomp_scratch_bytes_ctx)
  * and the part list of split bodies (36 B per part, n + 4096 parts). */
 size_t rpgpu_decomp_scratch_bytes(uint32_t n);
+/* The same for a context's rpgpu_opts.decomp_ws_lanes (never more than
+ * rpgpu_decomp_scratch_bytes(n)); the scratch of a context's decompress calls
+ * must hold at least this. */
+size_t rpgpu_decomp_scratch_bytes_ctx(const rpgpu_ctx* ctx, uint32_t n);
 /* Plan: per-batch output slots and their exclusive scan into d_scratch;
  * *d_out_bytes = output bytes needed.  The output buffer must hold
  * *d_out_bytes + RPGPU_ARENA_TAIL_PAD bytes. */

@@ -58,7 +58,7 @@ RPGPU_OK = 0
 RPGPU_PENDING = 1
 RPGPU_EINVAL = -1
 RPGPU_ECAPACITY = -4
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 DESC_NULL_RECORDS = 1  # rpgpu_batch_desc.flags
 
@@ -167,7 +167,7 @@ class GenSpec(C.Structure):
 
 class Opts(C.Structure):  # rpgpu_opts
     _fields_ = [("flags", C.c_uint32), ("max_batches", C.c_uint32), ("max_arena", C.c_uint64),
-                ("max_decoded_batch", C.c_uint64)]
+                ("max_decoded_batch", C.c_uint64), ("decomp_ws_lanes", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 DEFAULT_MAX_DECODED_BATCH = 64 << 20
@@ -247,6 +247,7 @@ def lib() -> C.CDLL:
             _LIB = L
             return _LIB
         _sig(L.rpgpu_decomp_scratch_bytes, C.c_size_t, _u32)
+        _sig(L.rpgpu_decomp_scratch_bytes_ctx, C.c_size_t, _vp, _u32)
         _sig(L.rpgpu_decomp_plan_device, _i32, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp)
         _sig(L.rpgpu_decomp_run_device, _i32, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp,
              _u64, _vp, _vp, _vp)
@@ -290,7 +291,7 @@ EXPORTED = [
     "rpgpu_validate_scratch_bytes", "rpgpu_validate_device", "rpgpu_plan_device",
     "rpgpu_run_device", "rpgpu_crc32c_ranges_device",
     "rpgpu_crc32c_extend", "rpgpu_internal_header_only_crc", "rpgpu_crc_record_batch",
-    "rpgpu_decomp_scratch_bytes", "rpgpu_decomp_plan_device", "rpgpu_decomp_run_device",
+    "rpgpu_decomp_scratch_bytes", "rpgpu_decomp_scratch_bytes_ctx", "rpgpu_decomp_plan_device", "rpgpu_decomp_run_device",
     "rpgpu_uncompress", "rpgpu_decompress_batch", "rpgpu_record_sets_scratch_bytes", "rpgpu_record_sets_plan_device",
     "rpgpu_record_sets_run_device", "rpgpu_segment_index_device",
 ]

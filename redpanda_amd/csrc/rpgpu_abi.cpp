@@ -35,7 +35,7 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
                       rpgpu_batch_result* d_res, rpgpu_record_index* d_index, uint64_t index_cap,
                       const void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s,
                       const Overlap* ov);
-size_t decomp_scratch_bytes(uint32_t n);
+size_t decomp_scratch_bytes(uint32_t n, uint32_t ws_cap);
 hipError_t validate_occupancy(int* blocks_per_cu);
 hipError_t launch_segment_index(const rpgpu_batch_desc* d_descs, const rpgpu_batch_result* d_res,
                                 const rpgpu_segment* d_segs, uint32_t nsegs, rpgpu_segment_state* d_states,
@@ -50,12 +50,12 @@ hipError_t launch_sets_run(const rpgpu_batch_desc* d_sets, uint32_t n, const uin
                            int grid, hipStream_t s, const Overlap* ov);
 hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                               const rpgpu_batch_result* d_vres, uint64_t* d_out_bytes, void* d_scratch,
-                              uint64_t max_decoded, hipStream_t s);
+                              uint64_t max_decoded, uint32_t ws_cap, hipStream_t s);
 hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                              const rpgpu_batch_result* d_vres, rpgpu_decomp_result* d_dres, uint8_t* d_out,
                              uint64_t out_cap, rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_vres2,
                              rpgpu_record_index* d_index, uint64_t index_cap, uint64_t* d_index_used,
-                             void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s,
+                             void* d_scratch, const uint32_t* d_tables, int grid, uint32_t ws_cap, hipStream_t s,
                              const Overlap* ov, const DecompStreams* ds);
 hipError_t launch_uncompress_bound(uint32_t codec, const uint8_t* d_in, uint64_t n, uint64_t* d_res,
                                    hipStream_t s);
@@ -158,6 +158,7 @@ struct rpgpu_ctx {
     uint64_t next_ticket = 1;
     bool busy = false;  // one in-flight submission per context (shard-owned)
     uint64_t max_decoded = RPGPU_DEFAULT_MAX_DECODED_BATCH;  // opts.max_decoded_batch
+    uint32_t ws_lanes = 0;  // opts.decomp_ws_lanes (0: the default ceiling)
     int efd = -1;       // rpgpu_eventfd: signalled by a host function after each stage
     std::string err;
 };
@@ -195,6 +196,7 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
     rpgpu_ctx* c = new (std::nothrow) rpgpu_ctx();
     if (!c) return nullptr;
     if (opts && opts->max_decoded_batch) c->max_decoded = opts->max_decoded_batch;
+    if (opts) c->ws_lanes = opts->decomp_ws_lanes;
     c->device = device;
     if (hipSetDevice(device) != hipSuccess) {
         delete c;
@@ -472,7 +474,10 @@ int32_t rpgpu_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, uint32_t
     return RPGPU_OK;
 }
 
-size_t rpgpu_decomp_scratch_bytes(uint32_t n) { return rpgpu::decomp_scratch_bytes(n); }
+size_t rpgpu_decomp_scratch_bytes(uint32_t n) { return rpgpu::decomp_scratch_bytes(n, 0); }
+size_t rpgpu_decomp_scratch_bytes_ctx(const rpgpu_ctx* c, uint32_t n) {
+    return c ? rpgpu::decomp_scratch_bytes(n, c->ws_lanes) : 0;
+}
 
 int32_t rpgpu_decomp_plan_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, uint32_t n,
                                  const uint8_t* d_data, const rpgpu_batch_result* d_results,
@@ -480,7 +485,7 @@ int32_t rpgpu_decomp_plan_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, 
     if (!c || (n && (!d_descs || !d_data || !d_results || !d_scratch))) return RPGPU_EINVAL;
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     hipError_t e = rpgpu::launch_decomp_plan(d_descs, n, d_data, d_results, d_out_bytes, d_scratch,
-                                              c->max_decoded, s);
+                                              c->max_decoded, c->ws_lanes, s);
     if (e != hipSuccess) return fail(c, e, "decomp plan launch");
     return RPGPU_OK;
 }
@@ -497,7 +502,7 @@ int32_t rpgpu_decomp_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, u
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     hipError_t e = rpgpu::launch_decomp_run(d_descs, n, d_data, d_results, d_dres, d_out, out_cap, d_out_descs,
                                             d_out_results, d_index, d_index ? index_cap : 0, d_index_used,
-                                            d_scratch, c->d_tables, c->grid, s,
+                                            d_scratch, c->d_tables, c->grid, c->ws_lanes, s,
                                             c->have_overlap ? &c->overlap : nullptr,
                                             c->have_dstreams ? &c->dstreams : nullptr);
     if (e != hipSuccess) return fail(c, e, "decomp run launch");

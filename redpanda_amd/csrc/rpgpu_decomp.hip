@@ -79,10 +79,25 @@ bool zstd_hbm() {
     return v != 0;
 }
 constexpr uint32_t kGzipLanes = 32768;
-uint32_t zstd_lanes(uint32_t n) { return n < kZstdLanes ? n : kZstdLanes; }
-uint32_t gzip_lanes(uint32_t n) { return n < kGzipLanes ? n : kGzipLanes; }
-size_t ws_region(uint32_t n) {
-    return zstd_hbm() ? (size_t)zstd_lanes(n) * sizeof(LaneWsZ) : (size_t)gzip_lanes(n) * sizeof(rpinfl::Ws);
+// cap: the context's ceiling on workspace lanes (rpgpu_opts.decomp_ws_lanes;
+// 0 = the defaults above, never below kMinWsLanes): an arena whose zstd / gzip
+// batches are few gets a scratch without gigabytes of idle workspaces, and its
+// zstd / gzip lanes grid-stride over more batches each
+constexpr uint32_t kMinWsLanes = 256;
+uint32_t lane_cap(uint32_t cap, uint32_t dflt) {
+    if (cap == 0 || cap > dflt) return dflt;
+    return cap < kMinWsLanes ? kMinWsLanes : cap;
+}
+uint32_t zstd_lanes(uint32_t n, uint32_t cap) {
+    const uint32_t c = lane_cap(cap, kZstdLanes);
+    return n < c ? n : c;
+}
+uint32_t gzip_lanes(uint32_t n, uint32_t cap) {
+    const uint32_t c = lane_cap(cap, kGzipLanes);
+    return n < c ? n : c;
+}
+size_t ws_region(uint32_t n, uint32_t cap) {
+    return zstd_hbm() ? (size_t)zstd_lanes(n, cap) * sizeof(LaneWsZ) : (size_t)gzip_lanes(n, cap) * sizeof(rpinfl::Ws);
 }
 // lanes in flight for the lane decoders (tuning knobs for measurements:
 // RPGPU_LZ_LANES, RPGPU_ZSTD_LANES; the scratch is sized for zstd_lanes(n))
@@ -100,6 +115,7 @@ struct SplitPart {
     uint64_t out_off;                      // within the decoded body
     uint32_t out_cap, hdr;
 };
+constexpr uint32_t kSkipPart = 0xffffffffu;  // a reserved slot without a part
 // parts in flight: LZ4 parts in [0, cap / 2), snappy's in [cap / 2, cap)
 uint32_t part_cap(uint32_t n) { return 2 * ((n + 4096u) / 2); }
 struct Parts {
@@ -120,10 +136,10 @@ size_t parts_head(uint32_t n) {
 }
 size_t counter_offset(uint32_t n) { return (parts_head(n) + validate_scratch_bytes(n) + 255) & ~(size_t)255; }
 size_t zws_offset(uint32_t n) { return counter_offset(n) + 256 + (size_t)decomp_waves(n) * kLitScratch; }
-size_t parts_offset(uint32_t n) {
-    return (zws_offset(n) + ws_region(n) + 255) & ~(size_t)255;
+size_t parts_offset(uint32_t n, uint32_t cap) {
+    return (zws_offset(n) + ws_region(n, cap) + 255) & ~(size_t)255;
 }
-Parts parts(void* p, uint32_t n) {
+Parts parts(void* p, uint32_t n, uint32_t cap) {
     uint8_t* b = static_cast<uint8_t*>(p);
     Parts s;
     s.slot = reinterpret_cast<uint64_t*>(b);
@@ -137,14 +153,14 @@ Parts parts(void* p, uint32_t n) {
     s.lits = b + counter_offset(n) + 256;
     s.zws = reinterpret_cast<LaneWsZ*>(b + zws_offset(n));
     s.gws = reinterpret_cast<rpinfl::Ws*>(b + zws_offset(n));
-    s.parts = reinterpret_cast<SplitPart*>(b + parts_offset(n));
+    s.parts = reinterpret_cast<SplitPart*>(b + parts_offset(n, cap));
     s.pres = reinterpret_cast<int32_t*>(s.parts + part_cap(n));
     return s;
 }
 }  // namespace
 
-size_t decomp_scratch_bytes(uint32_t n) {
-    return parts_offset(n) + (size_t)part_cap(n) * (sizeof(SplitPart) + sizeof(int32_t));
+size_t decomp_scratch_bytes(uint32_t n, uint32_t ws_cap) {
+    return parts_offset(n, ws_cap) + (size_t)part_cap(n) * (sizeof(SplitPart) + sizeof(int32_t));
 }
 
 // slots above this go to the wave decoders (a lane's serial decode of a
@@ -202,15 +218,23 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
     uint32_t* __restrict__ wlist, uint32_t* __restrict__ sfirst, uint32_t* __restrict__ scount,
     SplitPart* __restrict__ parts, uint32_t pcap) {
     __shared__ uint64_t wsum[kScanBlock / 64];
+    __shared__ uint64_t psum[kScanBlock / 64];
+    __shared__ uint32_t pbase[2];
     const uint32_t i = blockIdx.x * kScanBlock + threadIdx.x;
     uint64_t sz = 0, need = 0;
-    bool over = false;
+    bool over = false, wanted = false;
+    uint32_t codec = 0, np = 0;
+    const uint8_t* b = nullptr;
+    uint64_t body = 0;
+    const uint32_t half = pcap / 2;
     if (i < n) {
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
-        if (decomp_wanted(d, v)) {  // codec 1..4 (validation rejects 5..7)
-            const uint64_t body = body_len(v);
-            const uint8_t* b = data + d.offset + kHeaderSize;
+        wanted = decomp_wanted(d, v);
+        codec = v.codec;
+        if (wanted) {  // codec 1..4 (validation rejects 5..7)
+            body = body_len(v);
+            b = data + d.offset + kHeaderSize;
             const uint64_t bound = v.codec == 1   ? slot[i]  // gzip_bound_kernel's count
                                    : v.codec == 4 ? rpzstd::bound(b, body)
                                                   : rpcodec::uncompress_bound(v.codec, b, body);
@@ -221,71 +245,83 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
                 need = bound < kOverCeiling ? bound : kOverCeiling - 1;
             }
         }
+        // large batches: LZ4 frames / snappy-java bodies with a split plan go
+        // to the part decoders (LZ4 parts at parts[0..), snappy's at
+        // parts[pcap / 2..)); the rest to the wave decoders
+        if (wanted && !over && (codec == 2 || codec == 3) && sz > kSplitMinSlot) {
+            auto none = [](uint32_t, uint32_t, uint64_t, uint64_t, uint64_t, uint64_t, uint32_t) {};
+            np = codec == 3 ? rpcodec::lz4f_split(b, body, half, none) : rpcodec::snappy_java_split(b, body, half, none);
+        }
     }
+    // exclusive scans within the workgroup: output slots, and the parts of
+    // both codecs (LZ4 in the low, snappy in the high 32 bits)
     const uint64_t span = sz;
+    const uint64_t pspan = codec == 3 ? (uint64_t)np : ((uint64_t)np << 32);
     const uint32_t l = lane_id();
-    uint64_t x = span;
+    uint64_t x = span, y = pspan;
 #pragma unroll
     for (int s = 1; s < 64; s <<= 1) {
         const uint32_t lo = __shfl_up((uint32_t)x, s, 64), hi = __shfl_up((uint32_t)(x >> 32), s, 64);
-        if (l >= (uint32_t)s) x += ((uint64_t)hi << 32) | lo;
+        const uint32_t plo = __shfl_up((uint32_t)y, s, 64), phi = __shfl_up((uint32_t)(y >> 32), s, 64);
+        if (l >= (uint32_t)s) {
+            x += ((uint64_t)hi << 32) | lo;
+            y += ((uint64_t)phi << 32) | plo;
+        }
     }
     const uint32_t wv = threadIdx.x >> 6;
-    if (l == 63) wsum[wv] = x;
+    if (l == 63) {
+        wsum[wv] = x;
+        psum[wv] = y;
+    }
     __syncthreads();
-    uint64_t wbase = 0;
-    for (uint32_t k = 0; k < wv; k++) wbase += wsum[k];
+    uint64_t wbase = 0, pwbase = 0;
+    for (uint32_t k = 0; k < wv; k++) {
+        wbase += wsum[k];
+        pwbase += psum[k];
+    }
+    if (threadIdx.x == kScanBlock - 1) {
+        // one reservation per codec per workgroup (a CAS per batch serialised
+        // thousands of split batches: 42 ms of C5's plan)
+        const uint64_t tot = pwbase + y;
+        pbase[0] = (uint32_t)tot ? atomicAdd(wcount + 2, (uint32_t)tot) : 0u;
+        pbase[1] = (uint32_t)(tot >> 32) ? atomicAdd(wcount + 3, (uint32_t)(tot >> 32)) : 0u;
+    }
+    __syncthreads();
     if (i < n) {
         slot[i] = over ? (kOverCeiling | need) : sz;
         local[i] = wbase + x - span;
-        // large batches: LZ4 frames / snappy-java bodies with a split plan go
-        // to the part decoders (LZ4 parts at parts[0..), snappy's at
-        // parts[pcap / 2..)); the rest to the wave decoders (zstd list at
-        // wlist[0..), LZ list at wlist[n..))
         uint32_t sf = 0, sc = 0;
-        if (!over && sz > (vres[i].codec == 4 ? lane_max(4) : kSplitMinSlot) && decomp_wanted(descs[i], vres[i])) {
-            const uint32_t c = vres[i].codec;
-            if (c == 2 || c == 3) {
-                const uint8_t* b = data + descs[i].offset + kHeaderSize;
-                const uint64_t body = body_len(vres[i]);
-                auto none = [](uint32_t, uint32_t, uint64_t, uint64_t, uint64_t, uint64_t, uint32_t) {};
-                const uint32_t half = pcap / 2;
-                const uint32_t np = c == 3 ? rpcodec::lz4f_split(b, body, half, none)
-                                           : rpcodec::snappy_java_split(b, body, half, none);
-                if (np) {
-                    // reserve np part slots only if they fit: a reservation that
-                    // overflowed would leave slots nobody writes
-                    uint32_t* const pc = wcount + (c == 3 ? 2 : 3);
-                    uint32_t k0 = __hip_atomic_load(pc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    bool fit = false;
-                    while (k0 + np <= half) {
-                        const uint32_t prev = atomicCAS(pc, k0, k0 + np);
-                        if (prev == k0) {
-                            fit = true;
-                            break;
-                        }
-                        k0 = prev;
-                    }
-                    if (fit) {
-                        SplitPart* const pp = parts + (c == 3 ? 0 : half) + k0;
-                        auto put = [&](uint32_t k, uint32_t kind, uint64_t io, uint64_t il, uint64_t oo, uint64_t oc,
-                                       uint32_t h) {
-                            SplitPart t;
-                            t.batch = i, t.kind = kind, t.in_off = (uint32_t)io, t.in_len = (uint32_t)il;
-                            t.out_off = oo, t.out_cap = (uint32_t)oc, t.hdr = h;
-                            pp[k] = t;
-                        };
-                        if (c == 3) rpcodec::lz4f_split(b, body, half, put);
-                        else rpcodec::snappy_java_split(b, body, half, put);
-                        sf = (c == 3 ? 0 : half) + k0;
-                        sc = np;
-                    }
+        if (np) {
+            const uint64_t pe = pwbase + y - pspan;  // exclusive prefix within the workgroup
+            const uint32_t k0 = (codec == 3 ? pbase[0] + (uint32_t)pe : pbase[1] + (uint32_t)(pe >> 32));
+            SplitPart* const pp = parts + (codec == 3 ? 0 : half);
+            if ((uint64_t)k0 + np <= half) {
+                auto put = [&](uint32_t k, uint32_t kind, uint64_t io, uint64_t il, uint64_t oo, uint64_t oc,
+                               uint32_t h) {
+                    SplitPart t;
+                    t.batch = i, t.kind = kind, t.in_off = (uint32_t)io, t.in_len = (uint32_t)il;
+                    t.out_off = oo, t.out_cap = (uint32_t)oc, t.hdr = h;
+                    pp[k0 + k] = t;
+                };
+                if (codec == 3) rpcodec::lz4f_split(b, body, half, put);
+                else rpcodec::snappy_java_split(b, body, half, put);
+                sf = (codec == 3 ? 0 : half) + k0;
+                sc = np;
+            } else {
+                // the reservation ran past the part list: the slots it holds
+                // below the end carry no part (part_kernel skips them), the
+                // batch goes to the wave decoder
+                for (uint32_t k = k0; k < half && k < k0 + np; k++) {
+                    SplitPart t;
+                    t.batch = i, t.kind = kSkipPart, t.in_off = t.in_len = 0;
+                    t.out_off = 0, t.out_cap = 0, t.hdr = 0;
+                    pp[k] = t;
                 }
             }
-            if (!sc && sz > lane_max(c)) {
-                if (c == 4) wlist[atomicAdd(wcount, 1u)] = i;
-                else if (c == 2 || c == 3) wlist[n + atomicAdd(wcount + 1, 1u)] = i;
-            }
+        }
+        if (wanted && !over && !sc && sz > lane_max(codec)) {
+            if (codec == 4) wlist[atomicAdd(wcount, 1u)] = i;
+            else if (codec == 2 || codec == 3) wlist[n + atomicAdd(wcount + 1, 1u)] = i;
         }
         sfirst[i] = sf;
         scount[i] = sc;
@@ -586,6 +622,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_
     const uint32_t lanes = gridDim.x * blockDim.x;
     for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < cnt; g += lanes) {
         const SplitPart t = parts[base + g];
+        if (t.kind == kSkipPart) continue;
         const uint64_t off = block_base[t.batch / kScanBlock] + local[t.batch];
         int32_t r = -2;
         if (off + slot[t.batch] <= out_cap) {
@@ -688,11 +725,11 @@ __global__ void decomp_counters_kernel(uint32_t* c, uint32_t run) {
 // ------------------------------------------------------------ launchers
 hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                               const rpgpu_batch_result* d_vres, uint64_t* d_out_bytes, void* d_scratch,
-                              uint64_t max_decoded, hipStream_t s) {
+                              uint64_t max_decoded, uint32_t ws_cap, hipStream_t s) {
     if (n == 0) return d_out_bytes ? hipMemsetAsync(d_out_bytes, 0, sizeof(uint64_t), s) : hipSuccess;
-    const Parts p = parts(d_scratch, n);
+    const Parts p = parts(d_scratch, n, ws_cap);
     const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
-    const uint32_t gl = gzip_lanes(n);
+    const uint32_t gl = gzip_lanes(n, ws_cap);
     gzip_bound_kernel<<<(gl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.gws);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -713,10 +750,10 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                              const rpgpu_batch_result* d_vres, rpgpu_decomp_result* d_dres, uint8_t* d_out,
                              uint64_t out_cap, rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_vres2,
                              rpgpu_record_index* d_index, uint64_t index_cap, uint64_t* d_index_used,
-                             void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s,
+                             void* d_scratch, const uint32_t* d_tables, int grid, uint32_t ws_cap, hipStream_t s,
                              const Overlap* ov, const DecompStreams* ds) {
     if (n == 0) return d_index_used ? hipMemsetAsync(d_index_used, 0, sizeof(uint64_t), s) : hipSuccess;
-    const Parts p = parts(d_scratch, n);
+    const Parts p = parts(d_scratch, n, ws_cap);
     const uint32_t nblk = (n + 255) / 256;
     decomp_counters_kernel<<<1, 64, 0, s>>>(p.counter, 1);
     hipError_t e = hipGetLastError();
@@ -781,12 +818,13 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (zstd_hbm()) {  // the HBM-workspace lane decoder
         static const uint32_t zs_lanes = env_lanes("RPGPU_ZSTD_LANES", kZstdLanes);
-        const uint32_t zl = n < zs_lanes ? n : zs_lanes;
+        const uint32_t zc = zstd_lanes(n, ws_cap);
+        const uint32_t zl = zc < zs_lanes ? zc : zs_lanes;
         ws_lane_kernel<4><<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
                                                              d_dres, d_out, out_cap, d_out_descs, p.zws);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    const uint32_t gl = gzip_lanes(n);
+    const uint32_t gl = gzip_lanes(n, ws_cap);
     ws_lane_kernel<1><<<(gl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
                                                          d_dres, d_out, out_cap, d_out_descs, p.gws);
     if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -30,10 +30,12 @@ def _stream(stream: int):
 class Engine:
     """One rpgpu context (one per Seastar shard x GPU in the reference's terms)."""
 
-    def __init__(self, device: int = 0, max_decoded_batch: int = 0, walk_overlap: bool = False):
-        """walk_overlap: RPGPU_OPT_WALK_OVERLAP (arenas of many small, similar batches)."""
+    def __init__(self, device: int = 0, max_decoded_batch: int = 0, walk_overlap: bool = False,
+                 decomp_ws_lanes: int = 0):
+        """walk_overlap: RPGPU_OPT_WALK_OVERLAP (arenas of many small, similar batches);
+        decomp_ws_lanes: rpgpu_opts.decomp_ws_lanes (0: the default ceiling)."""
         self._lib = abi.lib()
-        opts = abi.Opts(abi.OPT_WALK_OVERLAP if walk_overlap else 0, 0, 0, max_decoded_batch)
+        opts = abi.Opts(abi.OPT_WALK_OVERLAP if walk_overlap else 0, 0, 0, max_decoded_batch, decomp_ws_lanes, 0)
         self._ctx = self._lib.rpgpu_open(device, C.byref(opts))
         if not self._ctx:
             raise EngineError(f"rpgpu_open({device}) failed (no usable HIP device?)")
@@ -125,9 +127,9 @@ class Engine:
             raise EngineError(f"rpgpu_crc32c_ranges_device: {rc} {self.last_error()}")
 
     # -- decompression (rpgpu_decomp_plan_device / rpgpu_decomp_run_device) -------------
-    @staticmethod
-    def decomp_scratch_bytes(n: int) -> int:
-        return int(abi.lib().rpgpu_decomp_scratch_bytes(n))
+    def decomp_scratch_bytes(self, n: int) -> int:
+        """rpgpu_decomp_scratch_bytes_ctx: the scratch this context's decompress calls need."""
+        return int(self._lib.rpgpu_decomp_scratch_bytes_ctx(self._ctx, n))
 
     def decomp_plan_device(self, d_descs: int, n: int, d_data: int, d_results: int, d_out_bytes: int,
                            d_scratch: int, stream: int = 0) -> None:

@@ -218,6 +218,26 @@ def test_many_tiny_zstd_gzip(eng):
     assert ((v == abi.V_OK) & (codec == 1)).sum() > 131_072 // 2
 
 
+def test_few_workspace_lanes():
+    """rpgpu_opts.decomp_ws_lanes = 256 (an LZ4 reader's small scratch): a
+    mixed arena with 6,000 zstd / gzip batches still decodes exactly as the
+    oracle, each of the 256 workspace lanes taking ~20 frames in turn, and the
+    context's scratch is a fraction of the default one."""
+    from redpanda_amd import abi, engine
+
+    spec = engine.make_spec(seed=0x5EED0078, partitions=32, codec_mix=(1 << 4) | (1 << 1) | (1 << 3),
+                            body_min=100, body_max=20_000, ops=abi.OPS_PRODUCE | abi.OP_DECOMP,
+                            payload=abi.PAYLOAD_TEXT, corrupt_ppm=5_000, corrupt_mask=0x3FF)
+    data, descs = engine.build_arena(spec, 9000)
+    with engine.Engine(0, decomp_ws_lanes=256) as e:
+        n = 200_000
+        assert e.decomp_scratch_bytes(n) < abi.lib().rpgpu_decomp_scratch_bytes(n) // 4
+        got = e.decompress_arena(data, descs)
+    compare(got, data, descs)
+    v, codec = got["dres"]["verdict"], got["dres"]["codec"]
+    assert ((v == abi.V_OK) & ((codec == 4) | (codec == 1))).sum() > 5000
+
+
 def test_uncompress_scalar_mirror(eng):
     rng = np.random.default_rng(3)
     cases = []
