@@ -29,14 +29,21 @@ for f in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.cs
         tot[row["Counter_Name"]][name] += float(row["Counter_Value"])
         disp[row["Counter_Name"]][name].add(row["Dispatch_Id"])
 per = defaultdict(dict)
+plain = cfg in ("c1", "c2")  # uncompressed: one step's validate / walk chunks, nothing else counted
 for c in tot:
     for name, v in tot[c].items():
-        calls = 2 if ("validate_kernel" in name or "walk_kernel" in name) else 1
+        hot = "validate_kernel" in name or "walk_kernel" in name
+        if plain:
+            if hot:
+                per[c][name] = v  # every chunk dispatch of the one step (--steps 1 --warmup 0)
+            continue
+        calls = 2 if hot else 1
         per[c][name] = v / len(disp[c][name]) * calls
 fetch = sum(v * (2.0 if "validate_kernel" in k else 1.0) for k, v in per["FETCH_SIZE"].items()) * 1024
 write = sum(per["WRITE_SIZE"].values()) * 1024
 out = {"batches": nb,
-       "kernel": "every rpgpu:: kernel of one pipeline step",
+       "kernel": ("validate_kernel + walk_kernel of one step (all chunk dispatches)" if plain
+                  else "every rpgpu:: kernel of one pipeline step"),
        "fetch_bytes": int(fetch), "write_bytes": int(write),
        "hbm_bytes_per_launch": int(fetch + write),
        "raw_counters_kb_per_step": {c: dict(v) for c, v in per.items()},
