@@ -41,8 +41,8 @@ _L = None
 
 
 def build(force: bool = False) -> Path:
-    srcs = [HERE / f for f in ("crc32c.c", "batch.c", "codec.c", "decomp.c", "sets.c", "index.c", "rporacle.h",
-                               "Makefile")]
+    srcs = [HERE / f for f in ("crc32c.c", "batch.c", "codec.c", "decomp.c", "sets.c", "index.c", "parse.c",
+                               "compact.c", "fetch.c", "frag.cc", "rporacle.h", "Makefile")]
     if force or not LIB_PATH.exists() or any(s.stat().st_mtime > LIB_PATH.stat().st_mtime for s in srcs):
         r = subprocess.run(["make", "-C", str(HERE), "-s"], capture_output=True, text=True)
         if r.returncode != 0:
@@ -166,6 +166,23 @@ def uncompress(codec: int, data, cap: int | None = None) -> tuple[int, bytes]:
     n = C.c_size_t()
     v = lib().orc_uncompress(codec, a.ctypes.data if a.size else None, a.size, out.ctypes.data, cap,
                              C.byref(n))
+    return int(v), out[: min(n.value, cap)].tobytes()
+
+
+def uncompress_frag(codec: int, data, frags, cap: int | None = None) -> tuple[int, bytes]:
+    """orc_uncompress_frag: the reference's wrapper loop over an input iobuf
+    of fragments of the given sizes (test infrastructure, frag.cc)."""
+    a = _buf(data)
+    cap = cap if cap is not None else max(1 << 16, a.size * 300)
+    out = np.zeros(cap, dtype=np.uint8)
+    f = np.ascontiguousarray(np.asarray(frags, dtype=np.uint32))
+    n = C.c_size_t()
+    L = lib()
+    L.orc_uncompress_frag.restype = C.c_int32
+    L.orc_uncompress_frag.argtypes = [C.c_int, C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint32, C.c_void_p,
+                                      C.c_size_t, C.POINTER(C.c_size_t)]
+    v = L.orc_uncompress_frag(codec, a.ctypes.data if a.size else None, a.size, f.ctypes.data if f.size else None,
+                              f.size, out.ctypes.data, cap, C.byref(n))
     return int(v), out[: min(n.value, cap)].tobytes()
 
 

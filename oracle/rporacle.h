@@ -79,6 +79,10 @@ uint64_t orc_validate_arena(const rpgpu_batch_desc* descs, uint32_t n,
  * with *out_len = required size when known. */
 int32_t orc_uncompress(int codec, const uint8_t* in, size_t n, uint8_t* out,
                        size_t cap, size_t* out_len);
+/* The same over an input iobuf of nfrag fragments of sizes frag[] (frag.cc:
+ * the wrapper loops per fragment, snappy through its Source / iovec API). */
+int32_t orc_uncompress_frag(int codec, const uint8_t* in, size_t n, const uint32_t* frag, uint32_t nfrag,
+                            uint8_t* out, size_t cap, size_t* out_len);
 /* compress with the reference's settings (lz4_frame_compressor.cc:68-158,
  * stream_zstd.cc:89-151, snappy_java_compressor.cc:58-75). */
 int32_t orc_compress(int codec, const uint8_t* in, size_t n, uint8_t* out,
