@@ -476,6 +476,9 @@ RPC_HD int64_t lz4_block(E& em, const uint8_t* in, int64_t isz, uint8_t* out, in
 //     overwriting the previous one's overshoot).
 // Longer runs take lz4_block's copies.  Host-compiled by the differential
 // fuzz test (tests/native/codec_fuzz.cpp) against the oracle.
+#ifndef RPGPU_LZ4_WC  // write-combined output stores in lz4_block_lane
+#define RPGPU_LZ4_WC 1
+#endif
 struct V16 {
     uint64_t lo, hi;
 };
@@ -603,6 +606,10 @@ int32_t lz4_block_lane(const uint8_t* in, int32_t isz, uint8_t* out, int32_t oca
     int err;
     Win64 W;
     w64_load(W, in, 0, lim);
+#if RPGPU_LZ4_WC
+    V16 cur{0, 0};   // output [ca, op), not stored yet (op - ca < 16)
+    int32_t ca = 0;  // memory holds the output below ca
+#endif
     for (;;) {
         // keep the token and the fields after it inside the window
         if (ip >= W.pos + 32) {
@@ -674,10 +681,16 @@ int32_t lz4_block_lane(const uint8_t* in, int32_t isz, uint8_t* out, int32_t oca
         if (last || ll > 32 || (!pat && (ml > 32 || off < 16 * nch)) || op_m + ml + 15 > oend) {
             // exact copies: nothing is written past the block's capacity
             // (a split frame's next block may already be there)
+#if RPGPU_LZ4_WC
+            if (op > ca) st_part(out + ca, cur.lo, cur.hi, (uint64_t)(op - ca));
+#endif
             if (ll) copy_exact(out + op, in + ip_lit, (uint64_t)ll);
             if (last) return op + ll;
             match_exact(out + op_m, (uint64_t)off, (uint64_t)ml);
             op = op_m + ml;
+#if RPGPU_LZ4_WC
+            ca = op;
+#endif
             continue;
         }
         // one round trip: every load of the sequence, then its stores
@@ -688,6 +701,19 @@ int32_t lz4_block_lane(const uint8_t* in, int32_t isz, uint8_t* out, int32_t oca
         if (ll > 16) L1 = v16_ld(in + ip_lit + 16);
         if (off != 0 && rel < 0) A0 = v16_ld(src);
         if (!pat && nch > 1 && rel + 16 < 0) A1 = v16_ld(src + 16);
+#if RPGPU_LZ4_WC
+        if (op > ca && rel < 0) {
+            // source bytes in [ca, op) are still in `cur`: A0's byte d is output byte ca
+            const int32_t d = ca - op - rel;
+            if (d <= 0) A0 = v16_ext(cur, V16{0, 0}, (uint32_t)-d);
+            else if (d < 16) A0 = v16_merge(A0, v16_shl(cur, (uint32_t)d), (uint32_t)d);
+            if (!pat && nch > 1 && rel + 16 < 0) {  // here d >= 2
+                const int32_t d1 = d - 16;
+                if (d1 <= 0) A1 = v16_ext(cur, V16{0, 0}, (uint32_t)-d1);
+                else if (d1 < 16) A1 = v16_merge(A1, v16_shl(cur, (uint32_t)d1), (uint32_t)d1);
+            }
+        }
+#endif
         // 16 source bytes at literal-relative r: stored bytes (A) below the
         // literal run, the run's own bytes (registers) from it on
         const int32_t r0 = rel, r1 = rel + 16;
@@ -723,8 +749,27 @@ int32_t lz4_block_lane(const uint8_t* in, int32_t isz, uint8_t* out, int32_t oca
         }
         if (ll + ml <= 16) {
             // the whole sequence in one 16-byte store (most text sequences)
-            v16_st(out + op, ll ? v16_merge(L0, v16_shl(first, (uint32_t)ll), (uint32_t)ll) : first);
+            const V16 sq = ll ? v16_merge(L0, v16_shl(first, (uint32_t)ll), (uint32_t)ll) : first;
+#if RPGPU_LZ4_WC
+            // ... appended to `cur`; a store only when 16 bytes are complete
+            // (no store: the next sequence's loads wait for none)
+            const uint32_t f = (uint32_t)(op - ca);
+            const V16 comb = f ? v16_merge(cur, v16_shl(sq, f), f) : sq;
+            if (f + (uint32_t)(ll + ml) >= 16) {
+                v16_st(out + ca, comb);
+                cur = v16_ext(sq, V16{0, 0}, 16 - f);
+                ca += 16;
+            } else {
+                cur = comb;
+            }
+#else
+            v16_st(out + op, sq);
+#endif
         } else {
+#if RPGPU_LZ4_WC
+            if (op > ca) v16_st(out + ca, cur);  // wild: the stores below overwrite [op, ca + 16)
+            ca = op_m + ml;
+#endif
             if (ll > 0) v16_st(out + op, L0);
             if (ll > 16) v16_st(out + op + 16, L1);
             if (pat) {
