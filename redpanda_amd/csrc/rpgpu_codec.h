@@ -566,6 +566,13 @@ RPC_HD uint32_t w64_at(Win64& W, const uint8_t* in, int32_t p, int32_t need, int
     const uint32_t lo = w64_dword(W, q);
     return sh ? (lo >> sh) | (w64_dword(W, q + 1) << (32 - sh)) : lo;
 }
+// bytes of x (output offset xb) that lie in [pb, pb + 16) replaced by p's
+RPC_HD V16 v16_overlay(const V16& x, int32_t xb, const V16& p, int32_t pb) {
+    const int32_t e = pb - xb;  // x's byte e is p's byte 0
+    if (e >= 16 || e <= -16) return x;
+    if (e >= 0) return v16_merge(x, v16_shl(p, (uint32_t)e), (uint32_t)e);
+    return v16_merge(v16_ext(p, V16{0, 0}, (uint32_t)-e), x, (uint32_t)(16 + e));
+}
 RPC_HD uint32_t lz4_varlen64(Win64& W, const uint8_t* in, int32_t& ip, int32_t lencheck, bool initial_check,
                              int& err, int32_t lim) {
     uint32_t len = 0;
@@ -607,8 +614,8 @@ int32_t lz4_block_lane(const uint8_t* in, int32_t isz, uint8_t* out, int32_t oca
     Win64 W;
     w64_load(W, in, 0, lim);
 #if RPGPU_LZ4_WC
-    V16 cur{0, 0};   // output [ca, op), not stored yet (op - ca < 16)
-    int32_t ca = 0;  // memory holds the output below ca
+    V16 cur{0, 0}, cur1{0, 0};  // output [ca, op), not stored yet (op - ca < 32)
+    int32_t ca = 0;             // memory holds the output below ca
 #endif
     for (;;) {
         // keep the token and the fields after it inside the window
@@ -682,7 +689,12 @@ int32_t lz4_block_lane(const uint8_t* in, int32_t isz, uint8_t* out, int32_t oca
             // exact copies: nothing is written past the block's capacity
             // (a split frame's next block may already be there)
 #if RPGPU_LZ4_WC
-            if (op > ca) st_part(out + ca, cur.lo, cur.hi, (uint64_t)(op - ca));
+            if (op - ca >= 16) {
+                v16_st(out + ca, cur);
+                if (op - ca > 16) st_part(out + ca + 16, cur1.lo, cur1.hi, (uint64_t)(op - ca - 16));
+            } else if (op > ca) {
+                st_part(out + ca, cur.lo, cur.hi, (uint64_t)(op - ca));
+            }
 #endif
             if (ll) copy_exact(out + op, in + ip_lit, (uint64_t)ll);
             if (last) return op + ll;
@@ -703,15 +715,12 @@ int32_t lz4_block_lane(const uint8_t* in, int32_t isz, uint8_t* out, int32_t oca
         if (!pat && nch > 1 && rel + 16 < 0) A1 = v16_ld(src + 16);
 #if RPGPU_LZ4_WC
         if (op > ca && rel < 0) {
-            // source bytes in [ca, op) are still in `cur`: A0's byte d is output byte ca
-            const int32_t d = ca - op - rel;
-            if (d <= 0) A0 = v16_ext(cur, V16{0, 0}, (uint32_t)-d);
-            else if (d < 16) A0 = v16_merge(A0, v16_shl(cur, (uint32_t)d), (uint32_t)d);
-            if (!pat && nch > 1 && rel + 16 < 0) {  // here d >= 2
-                const int32_t d1 = d - 16;
-                if (d1 <= 0) A1 = v16_ext(cur, V16{0, 0}, (uint32_t)-d1);
-                else if (d1 < 16) A1 = v16_merge(A1, v16_shl(cur, (uint32_t)d1), (uint32_t)d1);
-            }
+            // source bytes in [ca, op) are still in cur | cur1 (bytes from op
+            // on are the literal run's, merged below)
+            const int32_t sb = op_m - off;
+            A0 = v16_overlay(v16_overlay(A0, sb, cur, ca), sb, cur1, ca + 16);
+            if (!pat && nch > 1 && rel + 16 < 0)
+                A1 = v16_overlay(v16_overlay(A1, sb + 16, cur, ca), sb + 16, cur1, ca + 16);
         }
 #endif
         // 16 source bytes at literal-relative r: stored bytes (A) below the
@@ -754,20 +763,28 @@ int32_t lz4_block_lane(const uint8_t* in, int32_t isz, uint8_t* out, int32_t oca
             // ... appended to `cur`; a store only when 16 bytes are complete
             // (no store: the next sequence's loads wait for none)
             const uint32_t f = (uint32_t)(op - ca);
-            const V16 comb = f ? v16_merge(cur, v16_shl(sq, f), f) : sq;
-            if (f + (uint32_t)(ll + ml) >= 16) {
-                v16_st(out + ca, comb);
-                cur = v16_ext(sq, V16{0, 0}, 16 - f);
-                ca += 16;
+            if (f < 16) {  // f + ll + ml < 32: nothing to store
+                cur = f ? v16_merge(cur, v16_shl(sq, f), f) : sq;
+                cur1 = v16_ext(sq, V16{0, 0}, 16 - f);
             } else {
-                cur = comb;
+                const uint32_t g = f - 16;
+                const V16 c1 = g ? v16_merge(cur1, v16_shl(sq, g), g) : sq;
+                if (f + (uint32_t)(ll + ml) >= 32) {
+                    v16_st(out + ca, cur);
+                    v16_st(out + ca + 16, c1);
+                    cur = v16_ext(sq, V16{0, 0}, 16 - g);
+                    ca += 32;
+                } else {
+                    cur1 = c1;
+                }
             }
 #else
             v16_st(out + op, sq);
 #endif
         } else {
 #if RPGPU_LZ4_WC
-            if (op > ca) v16_st(out + ca, cur);  // wild: the stores below overwrite [op, ca + 16)
+            if (op > ca) v16_st(out + ca, cur);  // wild: the stores below overwrite [op, ca + 32)
+            if (op > ca + 16) v16_st(out + ca + 16, cur1);
             ca = op_m + ml;
 #endif
             if (ll > 0) v16_st(out + op, L0);
