@@ -253,6 +253,8 @@ def main() -> int:
                     help="compare every batch of a decompress config with the oracle (default: on for c5)")
     ap.add_argument("--payload", default="text", choices=["text", "alnum"],
                     help="record payload of the compressed configs (text: Zipf words, alnum: random)")
+    ap.add_argument("--walk-chunks", type=int, default=0, help="rpgpu_opts.walk_chunks (tuning; 0 = default)")
+    ap.add_argument("--blocks-per-cu", type=int, default=0, help="rpgpu_opts.blocks_per_cu (tuning; 0 = default)")
     args = ap.parse_args()
 
     import torch
@@ -280,7 +282,8 @@ def main() -> int:
     if args.ops:
         spec.ops = args.ops
     # chunked checksum / walk overlap for the uniform uncompressed arenas (RPGPU_OPT_WALK_OVERLAP)
-    eng = engine.Engine(local, walk_overlap=not decompress, decomp_ws_lanes=cfg.get("ws_lanes", 0))
+    eng = engine.Engine(local, walk_overlap=not decompress, decomp_ws_lanes=cfg.get("ws_lanes", 0),
+                        walk_chunks=args.walk_chunks, blocks_per_cu=args.blocks_per_cu)
     chunks, P_total, part_shift, (plo, phi) = rank_chunks(cfg, rank, world, scaling, args.batches)
     n = sum(m for _, m in chunks)
 

@@ -190,8 +190,7 @@ typedef struct rpgpu_rp_header {
  * batches of similar size (the produce path: C2 4.94 vs 5.17 ms per 1M batches);
  * arenas holding large batches, whose record walks are long serial chains, run
  * slower (C5 499 vs 434 ms), because each chunk's walks then wait for the
- * previous chunk's longest one.  The environment variable RPGPU_OVERLAP=1 / 0
- * forces it on / off. */
+ * previous chunk's longest one. */
 #define RPGPU_OPT_WALK_OVERLAP 1u
 
 typedef struct rpgpu_opts {
@@ -212,7 +211,13 @@ typedef struct rpgpu_opts {
      * gzip batches (an LZ4 or snappy topic) sets a small value (minimum 256):
      * its zstd / gzip batches still decode, each lane taking more of them. */
     uint32_t decomp_ws_lanes;
-    uint32_t reserved;     /* 0 */
+    /* RPGPU_OPT_WALK_OVERLAP: chunks the arena is checksummed in (0 = 16;
+     * at most 256).  C2 (1M batches): 4 / 8 / 16 / 32 chunks 4.74 / 4.71 /
+     * 4.63 / 4.83 ms per step. */
+    uint16_t walk_chunks;
+    /* validate_kernel workgroups per CU of the persistent grid (0 = 8,
+     * capped by occupancy; at most 32). */
+    uint16_t blocks_per_cu;
 } rpgpu_opts;
 #define RPGPU_DEFAULT_MAX_DECODED_BATCH (64ull << 20)
 
@@ -652,7 +657,9 @@ int32_t rpgpu_remote_segment_parse_device(rpgpu_ctx* ctx, const uint8_t* d_data,
  * index entries, bytes of OK batches (size_bytes), sum of the computed CRCs,
  * and the last offset (max base_offset + last_offset_delta over OK batches,
  * -1 if none; storage/offset_assignment.h:25-28).  A partition-sharded run
- * (one GPU per partition range) gathers these to one rank. */
+ * (one GPU per partition range) gathers these to one rank.
+ * The calls of one context share its per-workgroup partial table: issue them
+ * on one stream (or order them with events), never on two streams at once. */
 int32_t rpgpu_partition_summaries_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_descs,
                                          const rpgpu_batch_result* d_results, uint32_t n, uint32_t part_lo,
                                          uint32_t nparts, int64_t* d_out, void* hip_stream);
@@ -711,7 +718,14 @@ int32_t rpgpu_compaction_keep_device(rpgpu_ctx* ctx, const uint8_t* d_data, cons
  * compressed batch (do_compaction's compress_batch, :253-284) is
  * rpgpu_compress_plan_device / run_device over the output.
  * Plan, then run, on the same stream: the plan sizes the output
- * (*d_out_bytes); keep is rpgpu_compaction_keep_device's d_keep. */
+ * (*d_out_bytes); keep is rpgpu_compaction_keep_device's d_keep.  The
+ * reference keeps a record when its offset_delta is among the deltas of the
+ * records should_keep() accepted (std::count, :174-178); a record is kept here
+ * by its own keep flag.  The two agree because rpgpu_compaction_keep_device's
+ * flags are a function of the record's offset, as should_keep is: records
+ * sharing an offset_delta share one flag (tests/test_compaction.py,
+ * duplicate-delta case).  A caller passing its own flags must keep that
+ * property. */
 enum rpgpu_compact_action {
     RPGPU_COMPACT_SKIPPED = 0,
     RPGPU_COMPACT_DROPPED = 1,

@@ -111,7 +111,12 @@ void orc_segment_parse(const uint8_t* data, const rpgpu_segment_read* rd, rpgpu_
         /* accept: consume_batch_start (:127-131), consume_records (:246-257) */
         if (reader) expected = last + 1;
         phys += (uint64_t)(int64_t)h.size_bytes;
-        if (accepted < rd->desc_cap) {
+        /* consume_batch_end constructs record_batch(tag_ctor_ng), whose
+         * attrs.compression() throws for codec 5..7 (model/record.h:283-300,
+         * 582-585): the exception escapes consume() and the batch is never
+         * produced (no descriptor), as in the remote reader below */
+        const int throws = reader && (h.attrs & 7) > 4 && body <= avail;
+        if (!throws && accepted < rd->desc_cap) {
             rpgpu_batch_desc* d = &descs[rd->desc_first + accepted];
             d->offset = rd->offset + pos;
             d->length = (uint32_t)(body > avail ? avail + HDR : body + HDR);
@@ -121,7 +126,7 @@ void orc_segment_parse(const uint8_t* data, const rpgpu_segment_read* rd, rpgpu_
             d->flags = 0;
             d->reserved = 0;
         }
-        accepted++;
+        if (!throws) accepted++;
         /* consume_one adds the batch's bytes whatever the body read returned (:228-235) */
         bytes_consumed += (uint64_t)(int64_t)h.size_bytes;
         if (body > avail) {
@@ -129,10 +134,7 @@ void orc_segment_parse(const uint8_t* data, const rpgpu_segment_read* rd, rpgpu_
             break;
         }
         pos += HDR + body;
-        if (reader && (h.attrs & 7) > 4) {
-            /* consume_batch_end constructs record_batch(tag_ctor_ng), whose
-             * attrs.compression() throws for codec 5..7 (model/record.h:283-300,
-             * 582-585): the exception escapes consume() */
+        if (throws) {
             codec_throw = 1;
             break;
         }

@@ -167,7 +167,8 @@ class GenSpec(C.Structure):
 
 class Opts(C.Structure):  # rpgpu_opts
     _fields_ = [("flags", C.c_uint32), ("max_batches", C.c_uint32), ("max_arena", C.c_uint64),
-                ("max_decoded_batch", C.c_uint64), ("decomp_ws_lanes", C.c_uint32), ("reserved", C.c_uint32)]
+                ("max_decoded_batch", C.c_uint64), ("decomp_ws_lanes", C.c_uint32), ("walk_chunks", C.c_uint16),
+                ("blocks_per_cu", C.c_uint16)]
 
 
 DEFAULT_MAX_DECODED_BATCH = 64 << 20

@@ -208,13 +208,9 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
         return nullptr;
     }
     c->cu_count = prop.multiProcessorCount;
-    // kBlocksPerCU workgroups per CU (RPGPU_BLOCKS_PER_CU overrides, for
-    // tuning runs)
+    // kBlocksPerCU workgroups per CU unless opts.blocks_per_cu says otherwise
     int bpc = rpgpu::kBlocksPerCU;
-    if (const char* e = getenv("RPGPU_BLOCKS_PER_CU")) {
-        const int v = atoi(e);
-        if (v >= 1 && v <= 32) bpc = v;
-    }
+    if (opts && opts->blocks_per_cu >= 1 && opts->blocks_per_cu <= 32) bpc = opts->blocks_per_cu;
     // no more workgroups than fit at once (a persistent grid whose tail
     // waits for a free slot would serialise)
     int fit = 0;
@@ -227,10 +223,7 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
         return nullptr;
     }
     c->overlap.chunks = 16;  // C2 (1M batches): 4 / 8 / 16 / 32 chunks 4.74 / 4.71 / 4.63 / 4.83 ms, off 4.86
-    if (const char* e = getenv("RPGPU_RUN_CHUNKS")) {
-        const int v = atoi(e);
-        if (v >= 1 && v <= rpgpu::kMaxRunChunks) c->overlap.chunks = v;
-    }
+    if (opts && opts->walk_chunks >= 1 && opts->walk_chunks <= rpgpu::kMaxRunChunks) c->overlap.chunks = opts->walk_chunks;
     c->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     c->have_dstreams = hipStreamCreateWithFlags(&c->dstreams.aux, hipStreamNonBlocking) == hipSuccess &&
                        hipEventCreateWithFlags(&c->dstreams.fork, hipEventDisableTiming) == hipSuccess &&
@@ -240,9 +233,8 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
     for (int k = 0; c->have_overlap && k <= c->overlap.chunks; k++)
         c->have_overlap = hipEventCreateWithFlags(&c->overlap.ev[k], hipEventDisableTiming) == hipSuccess;
     // the walk of chunk k beside the checksums of chunk k + 1:
-    // RPGPU_OPT_WALK_OVERLAP, or RPGPU_OVERLAP=1 / 0 to force it on / off
-    bool want_overlap = opts && (opts->flags & RPGPU_OPT_WALK_OVERLAP);
-    if (const char* e = getenv("RPGPU_OVERLAP")) want_overlap = atoi(e) != 0;
+    // RPGPU_OPT_WALK_OVERLAP
+    const bool want_overlap = opts && (opts->flags & RPGPU_OPT_WALK_OVERLAP);
     if (!want_overlap) c->have_overlap = false;
     std::vector<uint32_t> t(rpgpu::kTableWords);
     rpgpu::build_tables(t.data());
@@ -808,11 +800,17 @@ int32_t rpgpu_decompress_batch(rpgpu_ctx* c, const void* batch, size_t len, int3
     const size_t room = cap > (size_t)RPGPU_HEADER_SIZE ? cap - RPGPU_HEADER_SIZE : 0;
     size_t blen = 0;
     const int32_t v = rpgpu_uncompress(c, codec, p + RPGPU_HEADER_SIZE, size - RPGPU_HEADER_SIZE,
-                                       static_cast<uint8_t*>(out) + RPGPU_HEADER_SIZE, room, &blen);
+                                       room ? static_cast<uint8_t*>(out) + RPGPU_HEADER_SIZE : nullptr, room, &blen);
     if (v < 0) return v;
     if (v != RPGPU_V_OK) {
         *out_len = v == RPGPU_V_DECOMP_OVERFLOW ? blen + RPGPU_HEADER_SIZE : 0;
         return v;
+    }
+    // the rewritten header needs its 61 bytes too (a body that decodes to
+    // nothing fits any room, a header does not: ADVICE r3)
+    if (cap < (size_t)RPGPU_HEADER_SIZE + blen) {
+        *out_len = RPGPU_HEADER_SIZE + blen;
+        return RPGPU_V_DECOMP_OVERFLOW;
     }
     rpgpu_rp_header h;
     memset(&h, 0, sizeof(h));

@@ -84,9 +84,13 @@ constexpr uint32_t kGzipLanes = 32768;
 // batches are few gets a scratch without gigabytes of idle workspaces, and its
 // zstd / gzip lanes grid-stride over more batches each
 constexpr uint32_t kMinWsLanes = 256;
+// (rounded up to whole 256-lane workgroups: the lane kernels launch
+// ceil(lanes / 256) workgroups and every thread below n owns a workspace --
+// a cap of 300 must not give threads 300..511 workspaces past the region,
+// ADVICE r3)
 uint32_t lane_cap(uint32_t cap, uint32_t dflt) {
     if (cap == 0 || cap > dflt) return dflt;
-    return cap < kMinWsLanes ? kMinWsLanes : cap;
+    return cap < kMinWsLanes ? kMinWsLanes : (cap + 255u) & ~255u;
 }
 uint32_t zstd_lanes(uint32_t n, uint32_t cap) {
     const uint32_t c = lane_cap(cap, kZstdLanes);

@@ -815,7 +815,11 @@ __global__ __launch_bounds__(kValidateThreads) void segment_parse_kernel(
             }
             if (reader) expected = last + 1;
             phys += sz;
-            if (accepted < rd.desc_cap && l == 0) {
+            // consume_batch_end's record_batch(tag_ctor_ng) throws for codec
+            // 5..7 (model/record.h:283-300,582-585): that batch is never
+            // produced, so it gets no descriptor (as in remote_parse_kernel)
+            const bool throws = reader && (H.byte(21) & 7u) > 4u && body <= avail;
+            if (!throws && accepted < rd.desc_cap && l == 0) {
                 rpgpu_batch_desc d;
                 d.offset = rd.offset + pos;
                 d.length = (uint32_t)(body > avail ? avail + kHeaderSize : body + kHeaderSize);
@@ -826,16 +830,14 @@ __global__ __launch_bounds__(kValidateThreads) void segment_parse_kernel(
                 d.reserved = 0;
                 descs[rd.desc_first + accepted] = d;
             }
-            accepted++;
+            if (!throws) accepted++;
             bytes_consumed += sz;
             if (body > avail) {
                 err = RPGPU_V_STREAM_SHORT;
                 break;
             }
             pos += kHeaderSize + body;
-            if (reader && (H.byte(21) & 7u) > 4u) {
-                // consume_batch_end's record_batch(tag_ctor_ng) throws for codec
-                // 5..7 (model/record.h:283-300,582-585)
+            if (throws) {
                 codec_throw = true;
                 break;
             }

@@ -22,14 +22,14 @@ pytestmark = pytest.mark.gpu
 OPS = 1 | 2 | 4 | 8 | 16  # CRC | HDRCRC | PARSE | INDEX | DECOMP
 
 
-def compare(got, data, descs):
+def compare(got, data, descs, nthreads=1):
     from redpanda_amd import abi
 
     res, dres = got["results"], got["dres"]
-    wres, _, _ = orc.validate_arena(data, descs)
+    wres, _, _ = orc.validate_arena(data, descs, nthreads=nthreads)
     assert np.array_equal(res.view(np.uint8), wres.view(np.uint8)), "validation results differ"
     caps = np.where(dres["out_cap"] > 0, dres["out_cap"].astype(np.int64) - 61 - 128, 0).astype(np.uint64)
-    want = orc.decompress_arena(data, descs, wres, caps, codecs=(1, 2, 3, 4))
+    want = orc.decompress_arena(data, descs, wres, caps, codecs=(1, 2, 3, 4), nthreads=nthreads)
     bad = np.nonzero(dres["verdict"] != want["verdicts"])[0]
     assert bad.size == 0, (f"decompress verdicts differ at {bad[:8]}: gpu {dres['verdict'][bad[:8]]} "
                            f"oracle {want['verdicts'][bad[:8]]}")
@@ -236,6 +236,45 @@ def test_few_workspace_lanes():
     compare(got, data, descs)
     v, codec = got["dres"]["verdict"], got["dres"]["codec"]
     assert ((v == abi.V_OK) & ((codec == 4) | (codec == 1))).sum() > 5000
+
+
+def test_ws_lanes_not_a_multiple_of_256():
+    """decomp_ws_lanes = 300 (not a whole number of 256-lane
+    workgroups) on a mixed zstd / gzip / LZ4 arena with split ~1 MiB LZ4
+    bodies and more batches than lanes: no workspace lies past the scratch's
+    workspace region (the cap is rounded up to 512 lanes), so the split parts
+    and their results beside it stay intact; every verdict, length and byte as
+    the oracle's."""
+    from redpanda_amd import abi, engine
+
+    spec = engine.make_spec(seed=0x5EED0079, partitions=32, codec_mix=(1 << 4) | (1 << 1) | (1 << 3),
+                            body_min=100, body_max=1 << 20, ops=abi.OPS_PRODUCE | abi.OP_DECOMP,
+                            payload=abi.PAYLOAD_TEXT, corrupt_ppm=5_000, corrupt_mask=0x3FF)
+    data, descs = engine.build_arena(spec, 1400)
+    with engine.Engine(0, decomp_ws_lanes=512) as e:
+        want_scratch = e.decomp_scratch_bytes(100_000)
+    with engine.Engine(0, decomp_ws_lanes=300) as e:
+        assert e.decomp_scratch_bytes(100_000) == want_scratch
+        got = e.decompress_arena(data, descs, runs=2)
+    compare(got, data, descs, nthreads=8)
+    v, codec = got["dres"]["verdict"], got["dres"]["codec"]
+    assert ((v == abi.V_OK) & ((codec == 4) | (codec == 1))).sum() > 600
+
+
+def test_decompress_batch_header_room(eng):
+    """rpgpu_decompress_batch with less room than the 61-byte
+    rewritten header (an empty LZ4 / zstd frame decodes to 0 bytes) reports
+    DECOMP_OVERFLOW with the capacity it needs instead of writing the header
+    past the caller's buffer."""
+    from redpanda_amd import abi
+
+    for codec in (3, 4):
+        b = batch(orc.compress(codec, b""), fmt=WIRE, record_count=0, attrs=codec)
+        for cap in (0, 1, 60):
+            gv, _, glen = eng.decompress_batch(b, WIRE, cap=cap)
+            assert gv == abi.V_DECOMP_OVERFLOW and glen == 61, (codec, cap, gv, glen)
+        gv, out, glen = eng.decompress_batch(b, WIRE, cap=61)
+        assert gv == abi.V_OK and glen == 61 and len(out) == 61
 
 
 def test_uncompress_scalar_mirror(eng):

@@ -193,6 +193,20 @@ def test_reader_offset_regression_throws():
     assert r["status"] == abi.V_READ_OFFSET_REGRESSION and r["accepted"] == 0
 
 
+def test_reader_codec_5_7_throws_without_producing_the_batch():
+    """consume_batch_end constructs record_batch(tag_ctor_ng), whose
+    attrs.compression() throws for codec 5..7 (model/record.h:283-300,582-585):
+    the batch is never produced, so the reader emits no descriptor for it; the
+    recovery consumer never builds a record_batch and accepts it."""
+    bs = seg_batches(4)
+    seg = b"".join(bs[:2]) + restamp_header(bs[2], attrs=6) + bs[3]
+    r, d, _ = one(seg, **R)
+    assert r["status"] == abi.V_BAD_CODEC_THROW and r["accepted"] == 2, r
+    assert list(d["length"]) == [len(bs[0]), len(bs[1])]
+    r, _, _ = one(seg)
+    assert r["status"] == abi.V_OK and r["accepted"] == 4
+
+
 # ---- GPU parity ---------------------------------------------------------------------------
 def corpus(rng):
     """Many segments: clean, truncated, fallocated, corrupted, garbage, reader configs."""
@@ -218,6 +232,9 @@ def corpus(rng):
             k = int(rng.integers(0, len(bs)))
             seg = b"".join(bs[:k]) + restamp_header(bs[k], size_bytes=int(rng.integers(-100, 100000))) + \
                 b"".join(bs[k + 1:])
+        elif kind == 6 and len(bs) > 1:  # codec bits 5..7 (throws in consume_batch_end for a reader)
+            k = int(rng.integers(0, len(bs)))
+            seg = b"".join(bs[:k]) + restamp_header(bs[k], attrs=int(rng.integers(5, 8))) + b"".join(bs[k + 1:])
         kw = {}
         if i % 3 == 1:
             kw = dict(mode=abi.PARSE_READER, start_offset=int(rng.integers(0, 1100)),
