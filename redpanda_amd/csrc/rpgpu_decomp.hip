@@ -39,7 +39,6 @@
 #include "rpgpu_zstd.h"
 #include "rpgpu_wave.h"
 #include "rpgpu_inflate.h"
-#include "rpgpu_lz4blk.h"  // block_part, kFallback
 
 namespace rpgpu {
 
@@ -114,20 +113,21 @@ uint32_t env_lanes(const char* name, uint32_t dflt) {
 uint32_t decomp_waves(uint32_t n) { return n < kDecompWaves ? n : kDecompWaves; }
 // scratch: slot[n] u64 | local[n] u64 | block_sum[nb] u64 | validate scratch |
 //          counters (256 B) | wave literal scratch[waves] | lane Ws[lanes]
-// parts in flight: LZ4 parts in [0, lz_cap), snappy's in [lz_cap, lz_cap + sn_cap)
-// (every LZ4 frame above kLz4SplitMin is split into its blocks: C3's
-// 262,144 batches are 262,144 parts; C5's ~1 MiB bodies 16 each; a body
-// whose parts do not fit goes to the wave decoder)
-uint32_t lz_cap(uint32_t n) { return n + 4096u; }
-uint32_t sn_cap(uint32_t n) { return (n + 4096u) / 2u; }
-uint32_t part_cap(uint32_t n) { return lz_cap(n) + sn_cap(n); }
+// one part of a split body (rpcodec::lz4f_split / snappy_java_split)
+struct SplitPart {
+    uint32_t batch, kind, in_off, in_len;  // offsets within the batch body
+    uint64_t out_off;                      // within the decoded body
+    uint32_t out_cap, hdr;
+};
+constexpr uint32_t kSkipPart = 0xffffffffu;  // a reserved slot without a part
+// parts in flight: LZ4 parts in [0, cap / 2), snappy's in [cap / 2, cap)
+uint32_t part_cap(uint32_t n) { return 2 * ((n + 4096u) / 2); }
 struct Parts {
     uint64_t *slot, *local, *block_sum;
     uint32_t* wlist;   // wave-owned batches: zstd [0, n), LZ [n, 2n)
     uint32_t *sfirst, *scount;  // a split batch's parts (scount 0: not split)
     SplitPart* parts;
     int32_t* pres;     // decoded size per part (-1 error, -2 no slot)
-    uint16_t* entries; // lz4_chain_kernel: chain entries of the LZ4 block parts
     void* vscratch;
     uint32_t* counter;
     uint8_t* lits;
@@ -159,15 +159,12 @@ Parts parts(void* p, uint32_t n, uint32_t cap) {
     s.gws = reinterpret_cast<rpinfl::Ws*>(b + zws_offset(n));
     s.parts = reinterpret_cast<SplitPart*>(b + parts_offset(n, cap));
     s.pres = reinterpret_cast<int32_t*>(s.parts + part_cap(n));
-    s.entries = reinterpret_cast<uint16_t*>(
-        (reinterpret_cast<uintptr_t>(s.pres + part_cap(n)) + 255) & ~(uintptr_t)255);
     return s;
 }
 }  // namespace
 
 size_t decomp_scratch_bytes(uint32_t n, uint32_t ws_cap) {
-    return parts_offset(n, ws_cap) + (size_t)part_cap(n) * (sizeof(SplitPart) + sizeof(int32_t)) + 256 +
-           lz4_entries_bytes(lz_cap(n));
+    return parts_offset(n, ws_cap) + (size_t)part_cap(n) * (sizeof(SplitPart) + sizeof(int32_t));
 }
 
 // slots above this go to the wave decoders (a lane's serial decode of a
@@ -185,14 +182,6 @@ __device__ __forceinline__ uint64_t lane_max(uint32_t codec) { return codec == 4
 #endif
 constexpr uint64_t kSplitMinSlot = RPGPU_SPLIT_MIN;
 static_assert(kSplitMinSlot <= kLaneMaxSlot, "split threshold above the lane decoders' limit");
-// LZ4 frames above this are split into their blocks, whatever their size:
-// 64 KiB blocks go to the workgroup block decoder (lz4_block_kernel), other
-// parts to the part lanes; smaller frames stay on the lane decoder (64 per
-// wave, no workgroup per few hundred bytes)
-#ifndef RPGPU_LZ4_SPLIT_MIN
-#define RPGPU_LZ4_SPLIT_MIN (16u << 10)
-#endif
-constexpr uint64_t kLz4SplitMin = RPGPU_LZ4_SPLIT_MIN;
 
 // slot[i] of a batch whose bound exceeds the per-batch ceiling: kOverCeiling |
 // bound -- no output reserved (the scan counts 0), verdict DECOMP_OVERFLOW
@@ -231,7 +220,7 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
     const rpgpu_batch_result* __restrict__ vres, uint64_t* __restrict__ slot, uint64_t* __restrict__ local,
     uint64_t* __restrict__ block_sum, uint64_t max_decoded, uint32_t* __restrict__ wcount,
     uint32_t* __restrict__ wlist, uint32_t* __restrict__ sfirst, uint32_t* __restrict__ scount,
-    SplitPart* __restrict__ parts, uint32_t lzc, uint32_t snc) {
+    SplitPart* __restrict__ parts, uint32_t pcap) {
     __shared__ uint64_t wsum[kScanBlock / 64];
     __shared__ uint64_t psum[kScanBlock / 64];
     __shared__ uint32_t pbase[2];
@@ -241,6 +230,7 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
     uint32_t codec = 0, np = 0;
     const uint8_t* b = nullptr;
     uint64_t body = 0;
+    const uint32_t half = pcap / 2;
     if (i < n) {
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
@@ -259,12 +249,12 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
                 need = bound < kOverCeiling ? bound : kOverCeiling - 1;
             }
         }
-        // LZ4 frames above kLz4SplitMin / large snappy-java bodies with a
-        // split plan go to the part decoders (LZ4 parts at parts[0..),
-        // snappy's at parts[lz_cap..)); the rest to the lane / wave decoders
-        if (wanted && !over && ((codec == 3 && sz > kLz4SplitMin) || (codec == 2 && sz > kSplitMinSlot))) {
+        // large batches: LZ4 frames / snappy-java bodies with a split plan go
+        // to the part decoders (LZ4 parts at parts[0..), snappy's at
+        // parts[pcap / 2..)); the rest to the wave decoders
+        if (wanted && !over && (codec == 2 || codec == 3) && sz > kSplitMinSlot) {
             auto none = [](uint32_t, uint32_t, uint64_t, uint64_t, uint64_t, uint64_t, uint32_t) {};
-            np = codec == 3 ? rpcodec::lz4f_split(b, body, lzc, none) : rpcodec::snappy_java_split(b, body, snc, none);
+            np = codec == 3 ? rpcodec::lz4f_split(b, body, half, none) : rpcodec::snappy_java_split(b, body, half, none);
         }
     }
     // exclusive scans within the workgroup: output slots, and the parts of
@@ -308,9 +298,8 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
         if (np) {
             const uint64_t pe = pwbase + y - pspan;  // exclusive prefix within the workgroup
             const uint32_t k0 = (codec == 3 ? pbase[0] + (uint32_t)pe : pbase[1] + (uint32_t)(pe >> 32));
-            const uint32_t cap = codec == 3 ? lzc : snc;
-            SplitPart* const pp = parts + (codec == 3 ? 0 : lzc);
-            if ((uint64_t)k0 + np <= cap) {
+            SplitPart* const pp = parts + (codec == 3 ? 0 : half);
+            if ((uint64_t)k0 + np <= half) {
                 auto put = [&](uint32_t k, uint32_t kind, uint64_t io, uint64_t il, uint64_t oo, uint64_t oc,
                                uint32_t h) {
                     SplitPart t;
@@ -318,15 +307,15 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
                     t.out_off = oo, t.out_cap = (uint32_t)oc, t.hdr = h;
                     pp[k0 + k] = t;
                 };
-                if (codec == 3) rpcodec::lz4f_split(b, body, cap, put);
-                else rpcodec::snappy_java_split(b, body, cap, put);
-                sf = (codec == 3 ? 0 : lzc) + k0;
+                if (codec == 3) rpcodec::lz4f_split(b, body, half, put);
+                else rpcodec::snappy_java_split(b, body, half, put);
+                sf = (codec == 3 ? 0 : half) + k0;
                 sc = np;
             } else {
                 // the reservation ran past the part list: the slots it holds
                 // below the end carry no part (part_kernel skips them), the
                 // batch goes to the wave decoder
-                for (uint32_t k = k0; k < cap && k < k0 + np; k++) {
+                for (uint32_t k = k0; k < half && k < k0 + np; k++) {
                     SplitPart t;
                     t.batch = i, t.kind = kSkipPart, t.in_off = t.in_len = 0;
                     t.out_off = 0, t.out_cap = 0, t.hdr = 0;
@@ -626,20 +615,18 @@ __global__ __launch_bounds__(64) void decomp_wave_kernel(
 // The parts of split batches, one lane each (CODEC 3: LZ4 blocks, 2: snappy
 // chunks); every part writes only its own output range, so they run in any
 // order.  A batch whose slot does not fit the caller's buffer decodes nothing.
-// LZ4 parts that lz4_block_kernel decoded (64 KiB blocks it did not hand
-// back with kFallback) are skipped.
 template <uint32_t CODEC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_WAVES))) void part_kernel(
-    const SplitPart* __restrict__ parts, const uint32_t* __restrict__ pcount, uint32_t base, uint32_t cap,
+    const SplitPart* __restrict__ parts, const uint32_t* __restrict__ pcount, uint32_t pcap,
     const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data, const uint64_t* __restrict__ slot,
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base, uint8_t* __restrict__ out,
     uint64_t out_cap, int32_t* __restrict__ pres) {
-    const uint32_t cnt = *pcount < cap ? *pcount : cap;
+    const uint32_t half = pcap / 2, base = CODEC == 3 ? 0 : half;
+    const uint32_t cnt = *pcount < half ? *pcount : half;
     const uint32_t lanes = gridDim.x * blockDim.x;
     for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < cnt; g += lanes) {
         const SplitPart t = parts[base + g];
         if (t.kind == kSkipPart) continue;
-        if (CODEC == 3 && rplz4b::block_part(t.kind, t.out_cap) && pres[base + g] != rplz4b::kFallback) continue;
         const uint64_t off = block_base[t.batch / kScanBlock] + local[t.batch];
         int32_t r = -2;
         if (off + slot[t.batch] <= out_cap) {
@@ -726,14 +713,13 @@ __global__ __launch_bounds__(64) void uncompress_one_kernel(uint32_t codec, cons
 
 // Queue counters (scratch `counter`): 0 / 1 LZ / zstd wave queue heads, 2 / 3
 // zstd / LZ wave list lengths, 4 / 5 LZ4 / snappy parts, 6 the plan's LZ list
-// length, 7 lz4_block_kernel's part queue.  A run appends split fallbacks to the LZ list, so each run starts
+// length.  A run appends split fallbacks to the LZ list, so each run starts
 // from the plan's length (a plan may be run any number of times).
 __global__ void decomp_counters_kernel(uint32_t* c, uint32_t run) {
     if (threadIdx.x != 0) return;
     if (run) {
         c[0] = 0;
         c[1] = 0;
-        c[7] = 0;  // lz4_block_kernel's part queue
         c[3] = c[6];
     } else {
         c[6] = c[3];
@@ -756,7 +742,7 @@ hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const
     if ((e = hipMemsetAsync(p.counter + 2, 0, 4 * sizeof(uint32_t), s)) != hipSuccess) return e;
     decomp_caps_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
                                                  max_decoded, p.counter + 2, p.wlist, p.sfirst, p.scount, p.parts,
-                                                 lz_cap(n), sn_cap(n));
+                                                 part_cap(n));
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     decomp_counters_kernel<<<1, 64, 0, s>>>(p.counter, 0);
@@ -786,15 +772,8 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     // split batches: LZ4 parts ahead of the lane kernels on the main stream,
     // snappy parts on the second, then their verdicts there (failures join
     // the LZ wave list); the two streams' chains come out about even
-    const uint32_t lzc = lz_cap(n), snc = sn_cap(n);
-    const uint32_t pgrid = (lzc < 65536u ? lzc + 255 : 65536u + 255) / 256;
-    const uint32_t sgrid = (snc < 65536u ? snc + 255 : 65536u + 255) / 256;
-    // 64 KiB LZ4 blocks: a workgroup each, in LDS; the other LZ4 parts (and
-    // the blocks it hands back) on part lanes after it
-    if ((e = launch_lz4_blocks(p.parts, p.counter + 4, lzc, d_descs, d_data, p.slot, p.local, p.block_sum, d_out,
-                               out_cap, p.pres, p.entries, p.counter + 7, s)) != hipSuccess)
-        return e;
-    part_kernel<3><<<pgrid, 256, 0, s>>>(p.parts, p.counter + 4, 0, lzc, d_descs, d_data, p.slot, p.local,
+    const uint32_t pgrid = (part_cap(n) / 2 < 65536u ? part_cap(n) / 2 + 255 : 65536u + 255) / 256;
+    part_kernel<3><<<pgrid, 256, 0, s>>>(p.parts, p.counter + 4, part_cap(n), d_descs, d_data, p.slot, p.local,
                                          p.block_sum, d_out, out_cap, p.pres);
     if (ds) {
         if ((e = hipEventRecord(ds->parts, s)) != hipSuccess) return e;
@@ -820,7 +799,7 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     decomp_wave_kernel<kFamZstd><<<decomp_waves(n), 64, sizeof(rpzstd::Ws), ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
                                                                 p.block_sum, d_dres, d_out, out_cap, d_out_descs,
                                                                 p.counter + 1, p.lits, p.wlist, p.counter + 2);
-    part_kernel<2><<<sgrid, 256, 0, ws>>>(p.parts, p.counter + 5, lzc, snc, d_descs, d_data, p.slot, p.local,
+    part_kernel<2><<<pgrid, 256, 0, ws>>>(p.parts, p.counter + 5, part_cap(n), d_descs, d_data, p.slot, p.local,
                                           p.block_sum, d_out, out_cap, p.pres);
     if (ds) {
         if ((e = hipStreamWaitEvent(ws, ds->parts, 0)) != hipSuccess) return e;

@@ -56,24 +56,6 @@ struct DecompStreams {
 
 void build_tables(uint32_t* out /* kTableWords */);
 
-// one part of a split compressed body (rpcodec::lz4f_split / snappy_java_split)
-struct SplitPart {
-    uint32_t batch, kind, in_off, in_len;  // offsets within the batch body
-    uint64_t out_off;                      // within the decoded body
-    uint32_t out_cap, hdr;
-};
-constexpr uint32_t kSkipPart = 0xffffffffu;  // a reserved slot without a part
-
-// lz4_chain_kernel + lz4_block_kernel (rpgpu_lz4blk.hip): the 64 KiB LZ4
-// block parts of [0, cap), one lane each for the chain entries (entries:
-// lz4_entries_bytes(cap)), then one workgroup each taken from *queue; results
-// in pres
-hipError_t launch_lz4_blocks(const SplitPart* parts, const uint32_t* pcount, uint32_t cap,
-                             const rpgpu_batch_desc* descs, const uint8_t* data, const uint64_t* slot,
-                             const uint64_t* local, const uint64_t* block_base, uint8_t* out, uint64_t out_cap,
-                             int32_t* pres, uint16_t* entries, uint32_t* queue, hipStream_t s);
-size_t lz4_entries_bytes(uint32_t parts);
-
 // Produce-handler verdict -> Kafka error code (produce.cc:440-489 in its
 // order: null records, legacy error, !valid_crc, !v2_format || !batch; then
 // batch_max_bytes, produce.cc:317-324).  Shared by the host and device entry points.
