@@ -211,12 +211,13 @@ typedef struct rpgpu_opts {
      * gzip batches (an LZ4 or snappy topic) sets a small value (minimum 256):
      * its zstd / gzip batches still decode, each lane taking more of them. */
     uint32_t decomp_ws_lanes;
-    /* RPGPU_OPT_WALK_OVERLAP: chunks the arena is checksummed in (0 = 16;
-     * at most 256).  C2 (1M batches): 4 / 8 / 16 / 32 chunks 4.74 / 4.71 /
-     * 4.63 / 4.83 ms per step. */
+    /* RPGPU_OPT_WALK_OVERLAP: 0 or 1 = checksums and record walks side by
+     * side over the whole arena (one launch each); k > 1 = the arena
+     * checksummed in k chunks, each chunk's walk beside the next chunk's
+     * checksums (at most 256). */
     uint16_t walk_chunks;
     /* validate_kernel workgroups per CU of the persistent grid (0 = 8,
-     * capped by occupancy; at most 32). */
+     * capped by occupancy; 5 beside a side-by-side walk; at most 32). */
     uint16_t blocks_per_cu;
 } rpgpu_opts;
 #define RPGPU_DEFAULT_MAX_DECODED_BATCH (64ull << 20)

@@ -222,8 +222,13 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
         delete c;
         return nullptr;
     }
-    c->overlap.chunks = 16;  // C2 (1M batches): 4 / 8 / 16 / 32 chunks 4.74 / 4.71 / 4.63 / 4.83 ms, off 4.86
+    // RPGPU_OPT_WALK_OVERLAP: checksums and walks side by side (1, the default)
+    // or chunked (walk_chunks > 1; C2 16 chunks: 4.29-4.42 ms per step, round 3)
+    c->overlap.chunks = 1;
     if (opts && opts->walk_chunks >= 1 && opts->walk_chunks <= rpgpu::kMaxRunChunks) c->overlap.chunks = opts->walk_chunks;
+    // side by side, the checksum grid leaves each SIMD room for a walk wave
+    c->overlap.grid = c->cu_count * (opts && opts->blocks_per_cu ? (int)opts->blocks_per_cu : rpgpu::kSideBlocksPerCU);
+    if (c->overlap.grid > c->grid) c->overlap.grid = c->grid;
     c->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     c->have_dstreams = hipStreamCreateWithFlags(&c->dstreams.aux, hipStreamNonBlocking) == hipSuccess &&
                        hipEventCreateWithFlags(&c->dstreams.fork, hipEventDisableTiming) == hipSuccess &&

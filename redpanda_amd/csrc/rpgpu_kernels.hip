@@ -102,6 +102,36 @@ __device__ __forceinline__ void write_result(rpgpu_batch_result* out, const Resu
     }
 }
 
+// The checksum side of the concurrent walk (rpgpu_walk.h): every dword but
+// the verdict (0) and index_count (15), then the handshake; if the walk is
+// already done, the final verdict and count too.
+__device__ __forceinline__ void write_result_side(rpgpu_batch_result* out, const Result& r, uint64_t* side,
+                                                  bool want) {
+    if (lane_id() == 0) {
+        const uint64_t bo = (uint64_t)r.h.base_offset, ft = (uint64_t)r.h.first_ts, mt = (uint64_t)r.h.max_ts;
+        uint32_t* w = reinterpret_cast<uint32_t*>(out);
+        w[1] = u32s(r.crc);
+        w[2] = u32s(r.crc_expected);
+        w[3] = u32s(r.header_crc);
+        u32x4 b = {u32s((uint32_t)r.h.size_bytes), u32s((uint32_t)r.h.record_count), u32s((uint32_t)bo),
+                   u32s((uint32_t)(bo >> 32))};
+        u32x4 c = {u32s((uint32_t)r.h.last_offset_delta),
+                   u32s((uint32_t)(uint16_t)r.h.attrs | ((uint32_t)(r.h.attrs & 7) << 16) |
+                        ((uint32_t)(uint8_t)r.h.type << 24)),
+                   u32s((uint32_t)ft), u32s((uint32_t)(ft >> 32))};
+        reinterpret_cast<u32x4*>(out)[1] = b;
+        reinterpret_cast<u32x4*>(out)[2] = c;
+        w[12] = u32s((uint32_t)mt);
+        w[13] = u32s((uint32_t)(mt >> 32));
+        w[14] = u32s(r.index_first);
+        const uint64_t old = atomicOr((unsigned long long*)side,
+                                      (unsigned long long)(kSideVDone | (want ? kSideWant : 0ull) |
+                                                           ((uint64_t)(uint8_t)r.verdict << 40)));
+        if (old & kSideWDone)
+            side_final(out, want ? (int32_t)(uint8_t)(old >> 32) : r.verdict, want ? (uint32_t)old : 0u);
+    }
+}
+
 __device__ __forceinline__ void load_tables(uint32_t* s, const uint32_t* __restrict__ g) {
     for (int i = threadIdx.x; i < kTableWords / 4; i += blockDim.x)
         reinterpret_cast<u32x4*>(s)[i] = reinterpret_cast<const u32x4*>(g)[i];
@@ -232,7 +262,7 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
                                               uint32_t b, const uint8_t* __restrict__ data,
                                               rpgpu_batch_result* __restrict__ res, uint32_t index_first,
                                               Prefetch& pf, const rpgpu_batch_desc& nd,
-                                              bool has_next DIAG_PARAM) {
+                                              bool has_next, uint64_t* __restrict__ side DIAG_PARAM) {
     const uint32_t l = lane_id();
     const uint8_t* p = data + d.offset;
     const uint32_t len = d.length;
@@ -369,7 +399,8 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
         // nothing of this batch is checksummed: just move the next one's rows
         load_rows(pf.x, nrs, ngm, 0, l);
         pf.gm = ngm;
-        write_result(res + b, r);
+        if (side) write_result_side(res + b, r, side + b, false);
+        else write_result(res + b, r);
         return;
     }
 
@@ -451,7 +482,11 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
     } else if (codec > 4) {
         r.verdict = RPGPU_V_BAD_CODEC_THROW;
     }
-    write_result(res + b, r);
+    if (side)
+        write_result_side(res + b, r, side + b,
+                          r.verdict == RPGPU_V_OK && codec == 0 && (d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX)));
+    else
+        write_result(res + b, r);
     STAMP(3);
 }
 
@@ -462,7 +497,8 @@ __global__ __launch_bounds__(kValidateThreads) void validate_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t b0, uint32_t n, const uint8_t* __restrict__ data,
     rpgpu_batch_result* __restrict__ res, rpgpu_record_index* __restrict__ index,
     const uint32_t* __restrict__ local_first, const uint32_t* __restrict__ caps,
-    const uint64_t* __restrict__ block_base, uint64_t index_cap, const uint32_t* __restrict__ tables) {
+    const uint64_t* __restrict__ block_base, uint64_t index_cap, const uint32_t* __restrict__ tables,
+    uint64_t* __restrict__ side) {
     __shared__ __attribute__((aligned(16))) uint32_t sT[kTableWords];
     load_tables(sT, tables);
     const uint32_t wave = threadIdx.x >> 6;
@@ -490,7 +526,7 @@ __global__ __launch_bounds__(kValidateThreads) void validate_kernel(
         // is lowered to scratch memory
         const rpgpu_batch_desc nd = sload_desc(descs + (has_next ? b + nw : b));
         const uint64_t first = sload(block_base + b / kScanBlock) + sload(local_first + b);
-        process_batch(sT, d, b, data, res, (uint32_t)first, pf, nd, has_next DIAG_PASS);
+        process_batch(sT, d, b, data, res, (uint32_t)first, pf, nd, has_next, side DIAG_PASS);
         STAMP(5);
     }
 #ifdef RPGPU_DIAG_STAMPS
@@ -540,6 +576,91 @@ __global__ __launch_bounds__(256) void walk_kernel(const rpgpu_batch_desc* __res
     walk_lanes(data, J, index, res);
 }
 
+// The walk side of the concurrent checksum / walk (rpgpu_walk.h handshake):
+// one lane per batch, the header read here (the checks validate_kernel makes
+// before and after the checksums, less the CRCs themselves), the records
+// walked for every batch those checks pass, uncompressed, whose ops ask for
+// a walk -- whatever its CRCs turn out to be; the checksum side decides
+// (kSideWant) whether the walk's verdict and entries count.
+__global__ __launch_bounds__(256) void walk_spec_kernel(const rpgpu_batch_desc* __restrict__ descs, uint32_t n,
+                                                        const uint8_t* __restrict__ data,
+                                                        rpgpu_batch_result* __restrict__ res,
+                                                        rpgpu_record_index* __restrict__ index,
+                                                        const uint32_t* __restrict__ local_first,
+                                                        const uint32_t* __restrict__ caps,
+                                                        const uint64_t* __restrict__ block_base, uint64_t index_cap,
+                                                        uint64_t* __restrict__ side) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    WalkJob J;
+    J.flags = 0;
+    J.body = 0;
+    J.base_offset = J.first_ts = 0;
+    J.n = J.first = J.cap = J.b = 0;
+    J.rc = 0;
+    if (b < n) {
+        const rpgpu_batch_desc d = descs[b];
+        const uint8_t* p = data + d.offset;
+        const uint32_t len = d.length;
+        if ((d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX)) && !(d.flags & RPGPU_DESC_NULL_RECORDS) &&
+            len >= (uint32_t)kHeaderSize) {
+            // the header (the arena is readable RPGPU_ARENA_TAIL_PAD bytes past any batch)
+            const u32x4 h0 = ld16(p), h1 = ld16(p + 16), h2 = ld16(p + 32), h3 = ld16(p + 48);
+            Img64 H;
+            H.w[0] = h0.x, H.w[1] = h0.y, H.w[2] = h0.z, H.w[3] = h0.w;
+            H.w[4] = h1.x, H.w[5] = h1.y, H.w[6] = h1.z, H.w[7] = h1.w;
+            H.w[8] = h2.x, H.w[9] = h2.y, H.w[10] = h2.z, H.w[11] = h2.w;
+            H.w[12] = h3.x, H.w[13] = h3.y, H.w[14] = h3.z, H.w[15] = h3.w;
+            bool ok;
+            uint32_t attrs, nb;
+            if (d.format == RPGPU_FMT_KAFKA_WIRE) {
+                // kafka_batch_adapter: magic 2, batch_length + 12 within the data
+                const uint64_t blen = (uint64_t)(int64_t)(int32_t)H.get_be(8, 4) + 12u;
+                ok = H.byte(16) == 2u && blen >= (uint64_t)kHeaderSize && blen <= (uint64_t)len;
+                nb = (uint32_t)blen;
+                attrs = (uint32_t)H.get_be(21, 2);
+                J.base_offset = (int64_t)H.get_be(0, 8);
+                J.first_ts = (int64_t)H.get_be(27, 8);
+                J.rc = (int32_t)H.get_be(57, 4);
+            } else {
+                // parser.cc read_header_impl: not all zero, size_bytes in [61, length]
+                uint32_t any = 0;
+#pragma unroll
+                for (int i = 0; i < 15; i++) any |= H.w[i];
+                any |= H.w[15] & 0xffu;
+                const int32_t sz = (int32_t)H.get_le(4, 4);
+                ok = any != 0 && sz >= kHeaderSize && (uint32_t)sz <= len;
+                nb = (uint32_t)sz;
+                attrs = (uint32_t)H.get_le(21, 2);
+                J.base_offset = (int64_t)H.get_le(8, 8);
+                J.first_ts = (int64_t)H.get_le(27, 8);
+                J.rc = (int32_t)H.get_le(57, 4);
+            }
+            if (ok && (attrs & 7u) == 0) {
+                const uint64_t first = block_base[b / kScanBlock] + local_first[b];
+                uint64_t cap = caps[b];
+                if (first >= index_cap) cap = 0;
+                else if (first + cap > index_cap) cap = index_cap - first;
+                J.body = d.offset + kHeaderSize;
+                J.n = nb - kHeaderSize;
+                J.first = (uint32_t)first;
+                J.cap = (uint32_t)cap;
+                J.b = b;
+                J.flags = kJobLive | ((d.ops & RPGPU_OP_INDEX) ? kJobIndex : 0u);
+            }
+        }
+    }
+    int32_t verdict;
+    uint32_t cnt;
+    walk_batch(data, J, index, verdict, cnt);
+    if (b < n) {
+        const uint64_t old = atomicOr((unsigned long long*)(side + b),
+                                      (unsigned long long)(kSideWDone | ((uint64_t)(uint8_t)verdict << 32) | cnt));
+        if (old & kSideVDone)
+            side_final(res + b, (old & kSideWant) ? verdict : (int32_t)(uint8_t)(old >> 40),
+                       (old & kSideWant) ? cnt : 0u);
+    }
+}
+
 // ------------------------------------------------------- index-cap prepass
 // Same rule as oracle/batch.c orc_index_cap.
 __device__ __forceinline__ uint32_t index_cap(const rpgpu_batch_desc& d, const uint8_t* data) {
@@ -576,7 +697,8 @@ __global__ __launch_bounds__(kScanBlock) void caps_kernel(const rpgpu_batch_desc
                                                           uint32_t n, const uint8_t* __restrict__ data,
                                                           uint32_t* __restrict__ caps,
                                                           uint32_t* __restrict__ local_first,
-                                                          uint64_t* __restrict__ block_sum) {
+                                                          uint64_t* __restrict__ block_sum,
+                                                          uint64_t* __restrict__ side) {
     __shared__ uint32_t wsum[kScanBlock / 64];
     const uint32_t i = blockIdx.x * kScanBlock + threadIdx.x;
     uint32_t cap = 0;
@@ -596,6 +718,7 @@ __global__ __launch_bounds__(kScanBlock) void caps_kernel(const rpgpu_batch_desc
     if (i < n) {
         caps[i] = cap;
         local_first[i] = wbase + x - cap;
+        side[i] = 0;  // launch_run's checksum / walk handshake
     }
     if (threadIdx.x == kScanBlock - 1) {
         uint64_t tot = 0;
@@ -1080,13 +1203,16 @@ hipError_t launch_kafka_codes(const rpgpu_batch_result* d_res, uint32_t n, uint3
 }
 
 // ------------------------------------------------------------ launchers
-// scratch layout: caps[n] u32 | local_first[n] u32 | block_sum[nb] u64
+// scratch layout: caps[n] u32 | local_first[n] u32 | block_sum[nb] u64 | side[n] u64
 static void scratch_parts(void* d_scratch, uint32_t n, uint32_t** caps, uint32_t** local_first,
-                          uint64_t** block_sum) {
+                          uint64_t** block_sum, uint64_t** side = nullptr) {
     uint8_t* sc = static_cast<uint8_t*>(d_scratch);
     *caps = reinterpret_cast<uint32_t*>(sc);
     *local_first = *caps + n;
-    *block_sum = reinterpret_cast<uint64_t*>(sc + (((size_t)n * 8 + 15) & ~(size_t)15));
+    const size_t o_bs = ((size_t)n * 8 + 15) & ~(size_t)15;
+    *block_sum = reinterpret_cast<uint64_t*>(sc + o_bs);
+    const size_t nb = (n + kScanBlock - 1) / kScanBlock;
+    if (side) *side = reinterpret_cast<uint64_t*>(sc + ((o_bs + nb * 8 + 63) & ~(size_t)63));
 }
 
 hipError_t launch_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
@@ -1097,9 +1223,9 @@ hipError_t launch_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_
     }
     const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
     uint32_t *caps, *local_first;
-    uint64_t* block_sum;
-    scratch_parts(d_scratch, n, &caps, &local_first, &block_sum);
-    caps_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, n, d_data, caps, local_first, block_sum);
+    uint64_t *block_sum, *side;
+    scratch_parts(d_scratch, n, &caps, &local_first, &block_sum, &side);
+    caps_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, n, d_data, caps, local_first, block_sum, side);
     block_scan_kernel<<<1, 1024, 0, s>>>(block_sum, nb, d_index_used);
     return hipGetLastError();
 }
@@ -1109,26 +1235,45 @@ hipError_t launch_block_scan(uint64_t* block_sum, uint32_t nb, uint64_t* total, 
     return hipGetLastError();
 }
 
-// The walk of a chunk of batches runs on the overlap stream while the next
-// chunk is checksummed: the walk is latency-bound, the checksum
-// bandwidth-bound, and the two share the CUs (validate_kernel leaves room:
-// kBlocksPerCU workgroups of 4 waves at <= 80 VGPRs).
+// Overlap (RPGPU_OPT_WALK_OVERLAP): either the checksums and the record
+// walks run side by side over the whole arena, one launch each on two
+// streams, finishing each batch through the rpgpu_walk.h handshake
+// (ov->chunks == 1: no grid boundaries), or the arena is checksummed in
+// ov->chunks launches and each chunk's walk runs on the overlap stream while
+// the next chunk is checksummed.  The walk is latency-bound, the checksum
+// bandwidth-bound; they share the CUs (ov->grid: a checksum grid that leaves
+// wave slots for the walk).
 hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                       rpgpu_batch_result* d_res, rpgpu_record_index* d_index, uint64_t index_cap,
                       const void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s,
                       const Overlap* ov) {
     if (n == 0) return hipSuccess;
     uint32_t *caps, *local_first;
-    uint64_t* block_sum;
-    scratch_parts(const_cast<void*>(d_scratch), n, &caps, &local_first, &block_sum);
-    const uint32_t chunks = (ov && n >= kRunChunkMin) ? (uint32_t)ov->chunks : 1u;
+    uint64_t *block_sum, *side;
+    scratch_parts(const_cast<void*>(d_scratch), n, &caps, &local_first, &block_sum, &side);
     hipError_t e = hipSuccess;
+    if (ov && n >= kRunChunkMin && ov->chunks == 1) {
+        if ((e = hipEventRecord(ov->ev[0], s)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(ov->aux, ov->ev[0], 0)) != hipSuccess) return e;
+        const uint32_t need = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+        const uint32_t vg = ov->grid > 0 ? (uint32_t)ov->grid : (uint32_t)grid;
+        validate_kernel<<<vg < need ? vg : need, kValidateThreads, 0, s>>>(d_descs, 0, n, d_data, d_res, d_index,
+                                                                            local_first, caps, block_sum, index_cap,
+                                                                            d_tables, side);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        walk_spec_kernel<<<(n + 255) / 256, 256, 0, ov->aux>>>(d_descs, n, d_data, d_res, d_index, local_first, caps,
+                                                               block_sum, index_cap, side);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if ((e = hipEventRecord(ov->ev[1], ov->aux)) != hipSuccess) return e;
+        return hipStreamWaitEvent(s, ov->ev[1], 0);
+    }
+    const uint32_t chunks = (ov && n >= kRunChunkMin) ? (uint32_t)ov->chunks : 1u;
     for (uint32_t k = 0; k < chunks; k++) {
         const uint32_t lo = (uint32_t)((uint64_t)n * k / chunks), hi = (uint32_t)((uint64_t)n * (k + 1) / chunks);
         const uint32_t need = (hi - lo + kWavesPerBlock - 1) / kWavesPerBlock;
         const uint32_t g = (uint32_t)grid < need ? (uint32_t)grid : need;
         validate_kernel<<<g, kValidateThreads, 0, s>>>(d_descs, lo, hi, d_data, d_res, d_index, local_first, caps,
-                                                        block_sum, index_cap, d_tables);
+                                                        block_sum, index_cap, d_tables, nullptr);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         hipStream_t ws = s;
         if (chunks > 1) {
@@ -1172,7 +1317,7 @@ hipError_t validate_occupancy(int* blocks_per_cu) {
 
 size_t validate_scratch_bytes(uint32_t n) {
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
-    return (((size_t)n * 8 + 15) & ~(size_t)15) + nb * 8 + 64;
+    return (((((size_t)n * 8 + 15) & ~(size_t)15) + nb * 8 + 63) & ~(size_t)63) + (size_t)n * 8 + 64;
 }
 
 }  // namespace rpgpu

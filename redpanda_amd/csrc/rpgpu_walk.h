@@ -127,11 +127,11 @@ __device__ __forceinline__ void store_entry(rpgpu_record_index* e, int64_t off, 
     dst[1] = b;
 }
 
-// Walks lane j's batch; writes its verdict and index_count into its result
-// (the rest of the result was written when the batch was checksummed).
-__device__ __forceinline__ void walk_lanes(const uint8_t* __restrict__ data, WalkJob J,
-                                        rpgpu_record_index* __restrict__ index,
-                                        rpgpu_batch_result* __restrict__ res) {
+// Walks lane j's batch: its record verdict and the index entries written
+// (min(records, cap); 0 without kJobIndex).
+__device__ __forceinline__ void walk_batch(const uint8_t* __restrict__ data, WalkJob J,
+                                           rpgpu_record_index* __restrict__ index, int32_t& verdict_out,
+                                           uint32_t& count_out) {
     bool live = (J.flags & kJobLive) != 0;
     const uint8_t* body = data + J.body;
     const int64_t n = J.n;
@@ -211,11 +211,39 @@ __device__ __forceinline__ void walk_lanes(const uint8_t* __restrict__ data, Wal
         cnt++;
         i++;
     }
+    verdict_out = verdict;
+    count_out = (J.flags & kJobIndex) ? (cnt < J.cap ? cnt : J.cap) : 0u;
+}
+
+// Walks lane j's batch; writes its verdict and index_count into its result
+// (the rest of the result was written when the batch was checksummed).
+__device__ __forceinline__ void walk_lanes(const uint8_t* __restrict__ data, WalkJob J,
+                                           rpgpu_record_index* __restrict__ index,
+                                           rpgpu_batch_result* __restrict__ res) {
+    int32_t verdict;
+    uint32_t cnt;
+    walk_batch(data, J, index, verdict, cnt);
     if (J.flags & kJobLive) {
         uint32_t* r = reinterpret_cast<uint32_t*>(res + J.b);
-        r[0] = (uint32_t)verdict;                                           // .verdict
-        r[15] = (J.flags & kJobIndex) ? (cnt < J.cap ? cnt : J.cap) : 0u;  // .index_count
+        r[0] = (uint32_t)verdict;  // .verdict
+        r[15] = cnt;               // .index_count
     }
+}
+
+// ---- concurrent checksum and walk (launch_run, Overlap::concurrent) -------
+// validate_kernel and walk_spec_kernel run side by side over the whole arena;
+// each batch's handshake word side[b] (zeroed by the plan) tells the second
+// of the two to finish: it alone writes the result's verdict and index_count
+// (dwords 0 and 15; the checksum side writes the other fourteen), so no two
+// writers ever store the same bytes.
+//   bits 0..31   walk: index entries written     bits 32..39 walk verdict
+//   bits 40..47  checksum verdict                bit 61 walk done
+//   bit 62       checksum done                   bit 63 the batch wants its walk
+constexpr uint64_t kSideWDone = 1ull << 61, kSideVDone = 1ull << 62, kSideWant = 1ull << 63;
+__device__ __forceinline__ void side_final(rpgpu_batch_result* r, int32_t verdict, uint32_t count) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(r);
+    w[0] = (uint32_t)verdict;
+    w[15] = count;
 }
 
 }  // namespace rpgpu

@@ -73,26 +73,29 @@ def test_crc32c_scalar_mirror(eng):
         assert eng.crc32c_extend(seed, b) == orc.crc32c(b, seed), n
 
 
-@pytest.mark.parametrize("case", ["headers", "ragged", "corrupt"])
-def test_walk_overlap_arenas(case):
+@pytest.mark.parametrize("chunks", [0, 16])
+@pytest.mark.parametrize("case", ["headers", "ragged", "corrupt", "disk_corrupt"])
+def test_walk_overlap_arenas(case, chunks):
     """RPGPU_OPT_WALK_OVERLAP on an arena above kRunChunkMin (16384 batches):
-    chunked checksums with each chunk's walk on a second stream.  Results and
-    index as the oracle's (uniform small batches, ragged ones whose walks
-    differ in length, and corrupted ones the walk must leave alone), on two
-    launches in a row."""
-    if case == "corrupt":
+    checksums and speculative walks side by side with the per-batch handshake
+    (chunks 0), or chunked checksums with each chunk's walk on a second stream
+    (16).  Results and index as the oracle's (uniform small batches, ragged
+    ones whose walks differ in length, corrupted ones -- wire and on-disk --
+    whose speculative walks must not count), on two launches in a row."""
+    if case in ("corrupt", "disk_corrupt"):
         kw = dict(CASES["headers"], corrupt_ppm=50_000, corrupt_mask=0x1FF)
     else:
         kw = dict(CASES[case])
     if case == "ragged":
         kw["body_max"] = 3000
-    spec = engine.make_spec(seed=zlib.crc32(case.encode()) + 7, format=abi.FMT_KAFKA_WIRE, **kw)
+    fmt = abi.FMT_RP_DISK if case == "disk_corrupt" else abi.FMT_KAFKA_WIRE
+    spec = engine.make_spec(seed=zlib.crc32(case.encode()) + 7, format=fmt, **kw)
     data, descs = engine.build_arena(spec, 20000)
-    with engine.Engine(0, walk_overlap=True) as e:
+    with engine.Engine(0, walk_overlap=True, walk_chunks=chunks) as e:
         got = e.submit(data, descs)
         again = e.submit(data, descs)
     want = orc.validate_arena(data, descs)
     assert_same(*got, *want)
     assert_same(*again, *want)
-    if case == "corrupt":
+    if case in ("corrupt", "disk_corrupt"):
         assert len(np.unique(want[0]["verdict"])) >= 4
