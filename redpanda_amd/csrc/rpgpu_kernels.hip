@@ -102,36 +102,6 @@ __device__ __forceinline__ void write_result(rpgpu_batch_result* out, const Resu
     }
 }
 
-// The checksum side of the concurrent walk (rpgpu_walk.h): every dword but
-// the verdict (0) and index_count (15), then the handshake; if the walk is
-// already done, the final verdict and count too.
-__device__ __forceinline__ void write_result_side(rpgpu_batch_result* out, const Result& r, uint64_t* side,
-                                                  bool want) {
-    if (lane_id() == 0) {
-        const uint64_t bo = (uint64_t)r.h.base_offset, ft = (uint64_t)r.h.first_ts, mt = (uint64_t)r.h.max_ts;
-        uint32_t* w = reinterpret_cast<uint32_t*>(out);
-        w[1] = u32s(r.crc);
-        w[2] = u32s(r.crc_expected);
-        w[3] = u32s(r.header_crc);
-        u32x4 b = {u32s((uint32_t)r.h.size_bytes), u32s((uint32_t)r.h.record_count), u32s((uint32_t)bo),
-                   u32s((uint32_t)(bo >> 32))};
-        u32x4 c = {u32s((uint32_t)r.h.last_offset_delta),
-                   u32s((uint32_t)(uint16_t)r.h.attrs | ((uint32_t)(r.h.attrs & 7) << 16) |
-                        ((uint32_t)(uint8_t)r.h.type << 24)),
-                   u32s((uint32_t)ft), u32s((uint32_t)(ft >> 32))};
-        reinterpret_cast<u32x4*>(out)[1] = b;
-        reinterpret_cast<u32x4*>(out)[2] = c;
-        w[12] = u32s((uint32_t)mt);
-        w[13] = u32s((uint32_t)(mt >> 32));
-        w[14] = u32s(r.index_first);
-        const uint64_t old = atomicOr((unsigned long long*)side,
-                                      (unsigned long long)(kSideVDone | (want ? kSideWant : 0ull) |
-                                                           ((uint64_t)(uint8_t)r.verdict << 40)));
-        if (old & kSideWDone)
-            side_final(out, want ? (int32_t)(uint8_t)(old >> 32) : r.verdict, want ? (uint32_t)old : 0u);
-    }
-}
-
 __device__ __forceinline__ void load_tables(uint32_t* s, const uint32_t* __restrict__ g) {
     for (int i = threadIdx.x; i < kTableWords / 4; i += blockDim.x)
         reinterpret_cast<u32x4*>(s)[i] = reinterpret_cast<const u32x4*>(g)[i];
@@ -262,7 +232,7 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
                                               uint32_t b, const uint8_t* __restrict__ data,
                                               rpgpu_batch_result* __restrict__ res, uint32_t index_first,
                                               Prefetch& pf, const rpgpu_batch_desc& nd,
-                                              bool has_next, uint64_t* __restrict__ side DIAG_PARAM) {
+                                              bool has_next DIAG_PARAM) {
     const uint32_t l = lane_id();
     const uint8_t* p = data + d.offset;
     const uint32_t len = d.length;
@@ -399,8 +369,7 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
         // nothing of this batch is checksummed: just move the next one's rows
         load_rows(pf.x, nrs, ngm, 0, l);
         pf.gm = ngm;
-        if (side) write_result_side(res + b, r, side + b, false);
-        else write_result(res + b, r);
+        write_result(res + b, r);
         return;
     }
 
@@ -482,11 +451,7 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
     } else if (codec > 4) {
         r.verdict = RPGPU_V_BAD_CODEC_THROW;
     }
-    if (side)
-        write_result_side(res + b, r, side + b,
-                          r.verdict == RPGPU_V_OK && codec == 0 && (d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX)));
-    else
-        write_result(res + b, r);
+    write_result(res + b, r);
     STAMP(3);
 }
 
@@ -497,8 +462,7 @@ __global__ __launch_bounds__(kValidateThreads) void validate_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t b0, uint32_t n, const uint8_t* __restrict__ data,
     rpgpu_batch_result* __restrict__ res, rpgpu_record_index* __restrict__ index,
     const uint32_t* __restrict__ local_first, const uint32_t* __restrict__ caps,
-    const uint64_t* __restrict__ block_base, uint64_t index_cap, const uint32_t* __restrict__ tables,
-    uint64_t* __restrict__ side) {
+    const uint64_t* __restrict__ block_base, uint64_t index_cap, const uint32_t* __restrict__ tables) {
     __shared__ __attribute__((aligned(16))) uint32_t sT[kTableWords];
     load_tables(sT, tables);
     const uint32_t wave = threadIdx.x >> 6;
@@ -526,7 +490,7 @@ __global__ __launch_bounds__(kValidateThreads) void validate_kernel(
         // is lowered to scratch memory
         const rpgpu_batch_desc nd = sload_desc(descs + (has_next ? b + nw : b));
         const uint64_t first = sload(block_base + b / kScanBlock) + sload(local_first + b);
-        process_batch(sT, d, b, data, res, (uint32_t)first, pf, nd, has_next, side DIAG_PASS);
+        process_batch(sT, d, b, data, res, (uint32_t)first, pf, nd, has_next DIAG_PASS);
         STAMP(5);
     }
 #ifdef RPGPU_DIAG_STAMPS
@@ -576,12 +540,12 @@ __global__ __launch_bounds__(256) void walk_kernel(const rpgpu_batch_desc* __res
     walk_lanes(data, J, index, res);
 }
 
-// The walk side of the concurrent checksum / walk (rpgpu_walk.h handshake):
-// one lane per batch, the header read here (the checks validate_kernel makes
-// before and after the checksums, less the CRCs themselves), the records
-// walked for every batch those checks pass, uncompressed, whose ops ask for
-// a walk -- whatever its CRCs turn out to be; the checksum side decides
-// (kSideWant) whether the walk's verdict and entries count.
+// The walk side of the concurrent checksum / walk (rpgpu_walk.h): one lane
+// per batch, the header read here (the checks validate_kernel makes before
+// and after the checksums, less the CRCs themselves), the records walked for
+// every batch those checks pass, uncompressed, whose ops ask for a walk --
+// whatever its CRCs turn out to be; walk_merge_kernel decides whether the
+// walk's verdict and entries count.
 __global__ __launch_bounds__(256) void walk_spec_kernel(const rpgpu_batch_desc* __restrict__ descs, uint32_t n,
                                                         const uint8_t* __restrict__ data,
                                                         rpgpu_batch_result* __restrict__ res,
@@ -652,12 +616,22 @@ __global__ __launch_bounds__(256) void walk_spec_kernel(const rpgpu_batch_desc* 
     int32_t verdict;
     uint32_t cnt;
     walk_batch(data, J, index, verdict, cnt);
-    if (b < n) {
-        const uint64_t old = atomicOr((unsigned long long*)(side + b),
-                                      (unsigned long long)(kSideWDone | ((uint64_t)(uint8_t)verdict << 32) | cnt));
-        if (old & kSideVDone)
-            side_final(res + b, (old & kSideWant) ? verdict : (int32_t)(uint8_t)(old >> 40),
-                       (old & kSideWant) ? cnt : 0u);
+    if (b < n) side[b] = side_word(verdict, cnt);
+}
+
+// After both: the walk's verdict and count for the batches that validated
+// OK, uncompressed, and ask for a walk (walk_kernel's condition).
+__global__ __launch_bounds__(256) void walk_merge_kernel(const rpgpu_batch_desc* __restrict__ descs, uint32_t n,
+                                                         rpgpu_batch_result* __restrict__ res,
+                                                         const uint64_t* __restrict__ side) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n) return;
+    const rpgpu_batch_result& r = res[b];
+    if ((descs[b].ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX)) && r.verdict == RPGPU_V_OK && r.codec == 0) {
+        const uint64_t w = side[b];
+        uint32_t* o = reinterpret_cast<uint32_t*>(res + b);
+        o[0] = (uint32_t)(int32_t)(uint8_t)(w >> 32);
+        o[15] = (uint32_t)w;
     }
 }
 
@@ -697,8 +671,7 @@ __global__ __launch_bounds__(kScanBlock) void caps_kernel(const rpgpu_batch_desc
                                                           uint32_t n, const uint8_t* __restrict__ data,
                                                           uint32_t* __restrict__ caps,
                                                           uint32_t* __restrict__ local_first,
-                                                          uint64_t* __restrict__ block_sum,
-                                                          uint64_t* __restrict__ side) {
+                                                          uint64_t* __restrict__ block_sum) {
     __shared__ uint32_t wsum[kScanBlock / 64];
     const uint32_t i = blockIdx.x * kScanBlock + threadIdx.x;
     uint32_t cap = 0;
@@ -718,7 +691,6 @@ __global__ __launch_bounds__(kScanBlock) void caps_kernel(const rpgpu_batch_desc
     if (i < n) {
         caps[i] = cap;
         local_first[i] = wbase + x - cap;
-        side[i] = 0;  // launch_run's checksum / walk handshake
     }
     if (threadIdx.x == kScanBlock - 1) {
         uint64_t tot = 0;
@@ -1223,9 +1195,9 @@ hipError_t launch_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_
     }
     const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
     uint32_t *caps, *local_first;
-    uint64_t *block_sum, *side;
-    scratch_parts(d_scratch, n, &caps, &local_first, &block_sum, &side);
-    caps_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, n, d_data, caps, local_first, block_sum, side);
+    uint64_t* block_sum;
+    scratch_parts(d_scratch, n, &caps, &local_first, &block_sum);
+    caps_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, n, d_data, caps, local_first, block_sum);
     block_scan_kernel<<<1, 1024, 0, s>>>(block_sum, nb, d_index_used);
     return hipGetLastError();
 }
@@ -1259,13 +1231,15 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
         const uint32_t vg = ov->grid > 0 ? (uint32_t)ov->grid : (uint32_t)grid;
         validate_kernel<<<vg < need ? vg : need, kValidateThreads, 0, s>>>(d_descs, 0, n, d_data, d_res, d_index,
                                                                             local_first, caps, block_sum, index_cap,
-                                                                            d_tables, side);
+                                                                            d_tables);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         walk_spec_kernel<<<(n + 255) / 256, 256, 0, ov->aux>>>(d_descs, n, d_data, d_res, d_index, local_first, caps,
                                                                block_sum, index_cap, side);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if ((e = hipEventRecord(ov->ev[1], ov->aux)) != hipSuccess) return e;
-        return hipStreamWaitEvent(s, ov->ev[1], 0);
+        if ((e = hipStreamWaitEvent(s, ov->ev[1], 0)) != hipSuccess) return e;
+        walk_merge_kernel<<<(n + 255) / 256, 256, 0, s>>>(d_descs, n, d_res, side);
+        return hipGetLastError();
     }
     const uint32_t chunks = (ov && n >= kRunChunkMin) ? (uint32_t)ov->chunks : 1u;
     for (uint32_t k = 0; k < chunks; k++) {
@@ -1273,7 +1247,7 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
         const uint32_t need = (hi - lo + kWavesPerBlock - 1) / kWavesPerBlock;
         const uint32_t g = (uint32_t)grid < need ? (uint32_t)grid : need;
         validate_kernel<<<g, kValidateThreads, 0, s>>>(d_descs, lo, hi, d_data, d_res, d_index, local_first, caps,
-                                                        block_sum, index_cap, d_tables, nullptr);
+                                                        block_sum, index_cap, d_tables);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         hipStream_t ws = s;
         if (chunks > 1) {

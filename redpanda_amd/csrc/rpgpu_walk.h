@@ -230,20 +230,15 @@ __device__ __forceinline__ void walk_lanes(const uint8_t* __restrict__ data, Wal
     }
 }
 
-// ---- concurrent checksum and walk (launch_run, Overlap::concurrent) -------
-// validate_kernel and walk_spec_kernel run side by side over the whole arena;
-// each batch's handshake word side[b] (zeroed by the plan) tells the second
-// of the two to finish: it alone writes the result's verdict and index_count
-// (dwords 0 and 15; the checksum side writes the other fourteen), so no two
-// writers ever store the same bytes.
-//   bits 0..31   walk: index entries written     bits 32..39 walk verdict
-//   bits 40..47  checksum verdict                bit 61 walk done
-//   bit 62       checksum done                   bit 63 the batch wants its walk
-constexpr uint64_t kSideWDone = 1ull << 61, kSideVDone = 1ull << 62, kSideWant = 1ull << 63;
-__device__ __forceinline__ void side_final(rpgpu_batch_result* r, int32_t verdict, uint32_t count) {
-    uint32_t* w = reinterpret_cast<uint32_t*>(r);
-    w[0] = (uint32_t)verdict;
-    w[15] = count;
+// ---- concurrent checksum and walk (launch_run, Overlap chunks == 1) --------
+// walk_spec_kernel runs beside validate_kernel over the whole arena and stores
+// each batch's walk as one word in side[b] (bits 0..31 index entries written,
+// 32..39 verdict); walk_merge_kernel then gives every batch that validated
+// OK, uncompressed, with a walk asked for, that verdict and count.  No
+// atomics: a returning atomic in the checksum wave would wait for the rows it
+// has in flight (one vmcnt for loads and stores on gfx9).
+__device__ __forceinline__ uint64_t side_word(int32_t verdict, uint32_t count) {
+    return ((uint64_t)(uint8_t)verdict << 32) | count;
 }
 
 }  // namespace rpgpu
