@@ -143,6 +143,8 @@ __device__ __forceinline__ void walk_batch(const uint8_t* __restrict__ data, Wal
     W.pos = 0;
     if (live) window_load(W, body, 0);
     rpgpu_record_index* idx = index + J.first;
+    u32x4 pa = {0, 0, 0, 0}, pe = {0, 0, 0, 0};  // an entry waiting for its pair
+    bool pend = false;
     while (wave_any(live)) {
         if (!live) continue;
         if (i >= J.rc) {  // record.h:686-690
@@ -204,12 +206,38 @@ __device__ __forceinline__ void walk_batch(const uint8_t* __restrict__ data, Wal
             live = false;
             continue;
         }
-        if ((J.flags & kJobIndex) && cnt < J.cap)
-            store_entry(idx + cnt, (int64_t)((uint64_t)J.base_offset + (uint64_t)(int64_t)(int32_t)off_delta),
-                        (int64_t)((uint64_t)J.first_ts + (uint64_t)ts_delta), (uint32_t)(key_off + kHeaderSize),
-                        (int32_t)klen, (uint32_t)(val_off + kHeaderSize), (int32_t)vlen);
+        if ((J.flags & kJobIndex) && cnt < J.cap) {
+            const uint64_t off = J.base_offset + (uint64_t)(int64_t)(int32_t)off_delta;
+            const uint64_t ts = (uint64_t)J.first_ts + (uint64_t)ts_delta;
+            const u32x4 a = {(uint32_t)off, (uint32_t)(off >> 32), (uint32_t)ts, (uint32_t)(ts >> 32)};
+            const u32x4 e = {(uint32_t)(key_off + kHeaderSize), (uint32_t)klen, (uint32_t)(val_off + kHeaderSize),
+                             (uint32_t)vlen};
+            // entries leave in aligned pairs (64 bytes): an even slot waits for
+            // its odd neighbour (32-byte stores to scattered half-lines were
+            // written back at 2.4x, profiles/r3/pmc_c2)
+            if (((J.first + cnt) & 1u) == 0) {
+                pa = a;
+                pe = e;
+                pend = true;
+            } else {
+                u32x4* dst = reinterpret_cast<u32x4*>(idx + cnt);
+                if (pend) {
+                    dst[-2] = pa;
+                    dst[-1] = pe;
+                }
+                dst[0] = a;
+                dst[1] = e;
+                pend = false;
+            }
+        }
         cnt++;
         i++;
+    }
+    if (pend) {  // the batch's last entry, alone in its pair
+        const uint32_t last = (cnt < J.cap ? cnt : J.cap) - 1;
+        u32x4* dst = reinterpret_cast<u32x4*>(idx + last);
+        dst[0] = pa;
+        dst[1] = pe;
     }
     verdict_out = verdict;
     count_out = (J.flags & kJobIndex) ? (cnt < J.cap ? cnt : J.cap) : 0u;
