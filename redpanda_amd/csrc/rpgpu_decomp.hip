@@ -32,8 +32,6 @@
 //                        Kafka CRC of the decompressed body, then the header
 //                        CRC over the header carrying it; record walk; index
 //   decomp_patch_kernel  stores both CRCs into the rewritten headers
-#include <stdlib.h>
-
 #include "rpgpu_device.h"  // before rpgpu_codec.h: HIP attributes
 #include "rpgpu_codec.h"
 #include "rpgpu_zstd.h"
@@ -61,23 +59,15 @@ constexpr uint64_t kLitScratch = (128u << 10) + 256;  // ZSTD_BLOCKSIZE_MAX + sl
 #define RPZ_LANES 131072  // 2 waves per SIMD at the lane kernel's VGPR count
 #endif
 constexpr uint32_t kZstdLanes = RPZ_LANES;
-union LaneWsZ {  // RPGPU_ZSTD_HBM: a zstd lane's workspace in HBM
+union LaneWsZ {  // a zstd (or gzip) lane's workspace in HBM
     rpzstd::Ws z;
     rpinfl::Ws g;
 };
-// zstd lanes keep their workspaces in HBM (the default) or, with
-// RPGPU_ZSTD_LDS=1, in LDS (zstd_lds_kernel: measured 3.25 s vs 0.585 s per C4
-// step -- the lane's chain of dependent global accesses per sequence, not its
-// table lookups, sets a lane's pace, and the LDS holds 20 lanes per CU against
-// 512 in HBM); gzip lanes keep theirs in HBM, 2 KB each for at most kGzipLanes
-// lanes (gzip is in no benchmark configuration)
-bool zstd_hbm() {
-    static const int v = [] {
-        const char* e = getenv("RPGPU_ZSTD_LDS");
-        return e && atoi(e) != 0 ? 0 : 1;
-    }();
-    return v != 0;
-}
+// zstd and gzip lanes keep their workspaces in HBM (one region, the union):
+// zstd tables in LDS, one workspace per lane, held 20 lanes per CU against
+// 512 in HBM and measured 3.25 s vs 0.585 s per C4 step (round 3: the lane's
+// chain of dependent global accesses per sequence, not its table lookups,
+// sets its pace); gzip is in no benchmark configuration
 constexpr uint32_t kGzipLanes = 32768;
 // cap: the context's ceiling on workspace lanes (rpgpu_opts.decomp_ws_lanes;
 // 0 = the defaults above, never below kMinWsLanes): an arena whose zstd / gzip
@@ -101,14 +91,8 @@ uint32_t gzip_lanes(uint32_t n, uint32_t cap) {
     return n < c ? n : c;
 }
 size_t ws_region(uint32_t n, uint32_t cap) {
-    return zstd_hbm() ? (size_t)zstd_lanes(n, cap) * sizeof(LaneWsZ) : (size_t)gzip_lanes(n, cap) * sizeof(rpinfl::Ws);
-}
-// lanes in flight for the lane decoders (tuning knobs for measurements:
-// RPGPU_LZ_LANES, RPGPU_ZSTD_LANES; the scratch is sized for zstd_lanes(n))
-uint32_t env_lanes(const char* name, uint32_t dflt) {
-    const char* e = getenv(name);
-    const long v = e ? atol(e) : 0;
-    return v > 0 && (uint64_t)v < dflt ? (uint32_t)v : dflt;
+    const size_t z = (size_t)zstd_lanes(n, cap) * sizeof(LaneWsZ), g = (size_t)gzip_lanes(n, cap) * sizeof(rpinfl::Ws);
+    return z > g ? z : g;
 }
 uint32_t decomp_waves(uint32_t n) { return n < kDecompWaves ? n : kDecompWaves; }
 // scratch: slot[n] u64 | local[n] u64 | block_sum[nb] u64 | validate scratch |
@@ -131,8 +115,8 @@ struct Parts {
     void* vscratch;
     uint32_t* counter;
     uint8_t* lits;
-    LaneWsZ* zws;     // zstd lanes (RPGPU_ZSTD_HBM) ...
-    rpinfl::Ws* gws;  // ... or gzip lanes: the same region
+    LaneWsZ* zws;     // zstd lanes ...
+    rpinfl::Ws* gws;  // ... and gzip lanes: the same region
 };
 size_t parts_head(uint32_t n) {
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
@@ -511,46 +495,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_WS_WA
     }
 }
 
-// zstd batches up to kZstdLaneMaxSlot: one lane per batch with its workspace in
-// LDS -- the compact form (rpzstd::WsC, ~7.6 KB: sequence FSE tables, the
-// first-level Huffman table and weight bands), so every table lookup of the
-// entropy decoders is an LDS access instead of a line of HBM (the HBM lane
-// workspaces cost ~35x the algorithmic bytes in traffic).  A
-// workgroup is one wave of which ZL lanes decode (the LDS holds ZL
-// workspaces); lanes stride over the arena's batches.
-#ifndef RPZ_LDS_LANES
-#define RPZ_LDS_LANES 5
-#endif
-constexpr uint32_t kZLdsLanes = RPZ_LDS_LANES;
-template <uint32_t ZL>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void zstd_lds_kernel(
-    const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
-    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
-    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
-    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
-    rpgpu_batch_desc* __restrict__ out_descs) {
-    __shared__ rpzstd::WsC wsl[ZL];
-    const uint32_t lid = threadIdx.x;
-    if (lid >= ZL) return;
-    rpzstd::WsC& ws = wsl[lid];
-    const uint32_t lanes = gridDim.x * ZL;
-    for (uint32_t i = blockIdx.x * ZL + lid; i < n; i += lanes) {
-        const rpgpu_batch_desc d = descs[i];
-        const rpgpu_batch_result v = vres[i];
-        uint64_t sz = slot[i];
-        if (!decomp_wanted(d, v) || v.codec != 4 || wave_owned(d, v, sz)) continue;
-        const uint64_t off = block_base[i / kScanBlock] + local[i];
-        int32_t verdict = RPGPU_V_SKIPPED;
-        uint64_t len = 0;
-        if (plan_slot(sz, off, out_cap, verdict, len)) {
-            rpzstd::DirectEmit em;
-            verdict = rpzstd::uncompress(em, data + d.offset + kHeaderSize, body_len(v), out + off + kHeaderSize,
-                                         sz - kHeaderSize - rpcodec::kSlack, &len, ws);
-        }
-        finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
-    }
-}
-
 // One batch body through the codec restatement, bytes produced by the wave.
 // K: the codec family a kernel instance decodes (kFamZstd: 4, kFamLz: 2 and 3).
 constexpr uint32_t kFamZstd = 4, kFamLz = 3;
@@ -778,24 +722,8 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     if (ds) {
         if ((e = hipEventRecord(ds->parts, s)) != hipSuccess) return e;
     }
-    // zstd first on the second stream: the LDS lane decoder (its workgroups
-    // hold the LDS; the LZ4 / snappy lane kernels on the main stream hold
-    // registers, so both fit the CUs at once), then the wave decoder for frames
-    // above kZstdLaneMaxSlot; neither waits for the parts
-    if (!zstd_hbm()) {
-        static int zgrid = 0;
-        if (!zgrid) {
-            int dev = 0, cus = 0, per = 0;
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, zstd_lds_kernel<kZLdsLanes>, 64, 0);
-            zgrid = (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
-        }
-        const uint32_t need = (n + kZLdsLanes - 1) / kZLdsLanes;
-        zstd_lds_kernel<kZLdsLanes><<<(uint32_t)zgrid < need ? (uint32_t)zgrid : need, 64, 0, ws>>>(
-            d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
+    // zstd frames above kZstdLaneMaxSlot first on the second stream (the wave
+    // decoder), then the snappy parts there
     decomp_wave_kernel<kFamZstd><<<decomp_waves(n), 64, sizeof(rpzstd::Ws), ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
                                                                 p.block_sum, d_dres, d_out, out_cap, d_out_descs,
                                                                 p.counter + 1, p.lits, p.wlist, p.counter + 2);
@@ -812,22 +740,16 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                                                               p.block_sum, d_dres, d_out, out_cap, d_out_descs,
                                                               p.counter, p.lits, p.wlist + n, p.counter + 3);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    static const uint32_t lz_lanes = env_lanes("RPGPU_LZ_LANES", 1u << 30);
-    const uint32_t lzl = n < lz_lanes ? n : lz_lanes;
-    const uint32_t lzb = (lzl + 255) / 256;
+    const uint32_t lzb = (n + 255) / 256;
     decomp_lane_kernel<3><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
                                               out_cap, d_out_descs, p.scount);
     decomp_lane_kernel<2><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
                                               out_cap, d_out_descs, p.scount);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (zstd_hbm()) {  // the HBM-workspace lane decoder
-        static const uint32_t zs_lanes = env_lanes("RPGPU_ZSTD_LANES", kZstdLanes);
-        const uint32_t zc = zstd_lanes(n, ws_cap);
-        const uint32_t zl = zc < zs_lanes ? zc : zs_lanes;
-        ws_lane_kernel<4><<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
-                                                             d_dres, d_out, out_cap, d_out_descs, p.zws);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
+    const uint32_t zl = zstd_lanes(n, ws_cap);  // the HBM-workspace lane decoder
+    ws_lane_kernel<4><<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres,
+                                                         d_out, out_cap, d_out_descs, p.zws);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t gl = gzip_lanes(n, ws_cap);
     ws_lane_kernel<1><<<(gl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
                                                          d_dres, d_out, out_cap, d_out_descs, p.gws);

@@ -256,30 +256,21 @@ RPC_HD bool huf_select_x2(uint64_t dst, uint64_t csrc) {
 }
 
 // ------------------------------------------------------------- workspace
-// Per-frame decoder state.  Two forms of one template:
-//   Ws  (kFull): the X1 Huffman table whole (4096 entries) -- per lane in HBM
-//        for the HBM lane decoder, LDS for the wave decoder and the scalar
-//        mirror: ~19 KB;
-//   WsC (compact, for workspaces in LDS one per lane): no X1 table; Huffman
-//        codes of up to kHuf1Log bits decode through huf1, longer ones from the
-//        code's weight band (hstart / hbase / hsym: the X1 table's layout
-//        without its copies, HUF_readDTableX1) -- ~7.6 KB.
-template <bool kFullHuf>
-struct WsT {
-    static constexpr bool kFull = kFullHuf;
-    uint16_t huf[kFullHuf ? (1u << kHufMaxLog) : 1];  // X1 table: symbol | nbBits << 8
+// Per-frame decoder state, ~19 KB: per lane in HBM for the lane decoder, in
+// LDS for the wave decoder and the scalar mirror.  (A compact ~7.6 KB form
+// without the X1 table, for one workspace per lane in LDS, measured 5.5x
+// slower per C4 step in round 3 and was removed.)
+struct Ws {
+    uint16_t huf[1u << kHufMaxLog];  // X1 table: symbol | nbBits << 8
     uint16_t huf1[1u << kHuf1Log];   // huf by the first kHuf1Log bits where that decides the code, else kHuf1None
     uint32_t ll[512], ml[512], of[256];  // sequence tables: state << 16 | nbBits << 8 | symbol
-    uint32_t llx[kFullHuf ? 512 : 1], mlx[kFullHuf ? 512 : 1];  // per state: baseline | extra bits << 24
+    uint32_t llx[512], mlx[512];     // per state: baseline | extra bits << 24
                                      // (ZSTD_seqSymbol's baseValue / nbAdditionalBits: no dependent
                                      // lookup per field; wave decoders only)
     uint32_t wt[64];                 // HUF weight FSE table: state << 16 | nbBits << 8 | symbol
     int16_t norm[256];
     uint16_t next[256];
     uint8_t w[256];                  // Huffman weights
-    uint8_t hsym[kFullHuf ? 1 : 256];  // WsC: symbols by (weight, symbol), the X1 table's order
-    uint16_t hstart[kHufMaxLog + 2];   // WsC: first X1 index of each weight
-    uint16_t hbase[kHufMaxLog + 2];    // WsC: first hsym index of each weight
     uint32_t rank[kHufMaxLog + 1];
     uint64_t rep[3];
     uint8_t ll_log, ml_log, of_log, huf_log;
@@ -288,8 +279,6 @@ struct WsT {
     uint64_t t_lit, t_seq, n_seq, n_lit;  // diagnostics build: clock64 per phase
 #endif
 };
-using Ws = WsT<true>;
-using WsC = WsT<false>;
 #if RPZ_PROF && defined(__HIP_DEVICE_COMPILE__)
 #define RPZ_CLK() ((uint64_t)clock64())
 #else
@@ -589,7 +578,7 @@ RPC_HD int64_t huf_read_table(W& w, const uint8_t* in, uint64_t n) {
     if (w.rank[1] < 2 || (w.rank[1] & 1)) return RPZ_FAIL(-1);
     const uint32_t nsym = (uint32_t)oSize + 1;
     // X1 table: ranks by weight ascending, symbols in order within a weight
-    if constexpr (W::kFull) {
+    {
         uint32_t start = 0;
         for (uint32_t r = 1; r <= log; r++) {
             const uint32_t cur = start;
@@ -611,34 +600,6 @@ RPC_HD int64_t huf_read_table(W& w, const uint8_t* in, uint64_t n) {
                 const uint16_t e = w.huf[i << (log - kHuf1Log)];
                 w.huf1[i] = (e >> 8) <= kHuf1Log ? e : kHuf1None;
             }
-    } else {
-        // the same layout without the copies: weight r's symbols occupy X1
-        // indexes [hstart[r], hstart[r + 1]), 2^(r-1) each, in symbol order
-        uint32_t start = 0, base = 0;
-        for (uint32_t r = 1; r <= log; r++) {
-            w.hstart[r] = (uint16_t)start;
-            w.hbase[r] = (uint16_t)base;
-            start += w.rank[r] << (r - 1);
-            base += w.rank[r];
-            w.rank[r] = w.hbase[r];
-        }
-        w.hstart[log + 1] = (uint16_t)start;
-        for (uint32_t s = 0; s < nsym; s++) {
-            const uint32_t wt = w.w[s];
-            if (wt) w.hsym[w.rank[wt]++] = (uint8_t)s;
-        }
-        w.huf_log = (uint8_t)log;
-        w.huf1_on = 1;
-        // huf1: the first min(log, kHuf1Log) bits; a code that fits decides
-        const uint32_t L1 = log < kHuf1Log ? log : kHuf1Log;
-        for (uint32_t i = 0; i < (1u << L1); i++) {
-            const uint32_t v = i << (log - L1);  // the X1 index of the first entry
-            uint32_t r = 1;
-            while (r < log && v >= w.hstart[r + 1]) r++;
-            const uint32_t nb = log + 1 - r;
-            w.huf1[i] = nb <= L1 ? (uint16_t)(w.hsym[w.hbase[r] + ((v - w.hstart[r]) >> (r - 1))] | (nb << 8))
-                                 : kHuf1None;
-        }
     }
     return (int64_t)iSize + 1;
 }
@@ -681,21 +642,12 @@ RPC_HD void huf_end(HufS& h) {
 // the X1 entry of the L-bit index v (two: through huf1 first)
 template <class W>
 RPC_HD uint32_t huf_entry(const W& w, uint32_t v, uint32_t L, bool two) {
-    if constexpr (W::kFull) {
-        if (two) {
-            const uint32_t t = w.huf1[v >> (L - kHuf1Log)];
-            if (t != kHuf1None) return t;
-        }
-        return w.huf[v];
-    } else {
-        if (L <= kHuf1Log) return w.huf1[v];
+    (void)L;
+    if (two) {
         const uint32_t t = w.huf1[v >> (L - kHuf1Log)];
         if (t != kHuf1None) return t;
-        // a code longer than kHuf1Log bits: weight r < L + 1 - kHuf1Log
-        uint32_t r = 1;
-        while (r + kHuf1Log < L && v >= w.hstart[r + 1]) r++;
-        return (uint32_t)w.hsym[w.hbase[r] + ((v - w.hstart[r]) >> (r - 1))] | ((L + 1 - r) << 8);
     }
+    return w.huf[v];
 }
 template <class W>
 RPC_HD void huf_step(const W& w, HufS& h, uint32_t L, bool x2, bool two = false) {
@@ -936,7 +888,6 @@ RPC_HD void build_default(uint32_t* t, uint16_t* next, int16_t* norm, const int8
 // ZSTD_buildSeqTable for one of LL / OF / ML.  Returns bytes or -1.
 template <class W>
 RPC_HD void seq_extra(W& w, uint32_t which) {
-    if constexpr (!W::kFull) return;
     if (which == 1) return;
     const uint32_t* t = which == 0 ? w.ll : w.ml;
     uint32_t* x = which == 0 ? w.llx : w.mlx;
@@ -998,7 +949,7 @@ template <class E, class W>
 RPZ_COLD int64_t block(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t fstart, uint64_t op,
                        uint64_t cap, uint64_t tail) {
     if (n >= kBlockMax) return RPZ_FAIL(-1);
-    constexpr bool kLdsWs = E::kInlineBlocks && W::kFull;  // the wave decoders keep Ws in LDS
+    constexpr bool kLdsWs = E::kInlineBlocks;  // the wave decoders keep Ws in LDS
     Lit lit;
 #if RPZ_PROF
     const uint64_t c0 = RPZ_CLK();

@@ -296,23 +296,6 @@ void compare(const Bytes& in) {
     uint64_t elen = 0;
     rpzstd::DirectEmit em;
     const int32_t ev = rpzstd::uncompress(em, ip, in.size(), eout.data(), cap, &elen, ws);
-    // the compact workspace (the LDS lane decoder's form) decides identically
-    {
-        static rpzstd::WsC wc;
-        Bytes cout(eout.size());
-        uint64_t clen = 0;
-        const int32_t cv = rpzstd::uncompress(em, ip, in.size(), cout.data(), cap, &clen, wc);
-        if (cv != ev || clen != elen || (ev == 0 && memcmp(cout.data(), eout.data(), elen))) {
-            fprintf(stderr, "case %ld: compact workspace v=%d len=%llu, full v=%d len=%llu\n", n_cases, cv,
-                    (unsigned long long)clen, ev, (unsigned long long)elen);
-            FILE* fp = fopen("zstd_fuzz_fail.bin", "wb");
-            if (fp) {
-                fwrite(in.data(), 1, in.size(), fp);
-                fclose(fp);
-            }
-            exit(1);
-        }
-    }
     static Bytes oout(96u << 20);
     size_t olen = 0;
     const int32_t ov = orc_uncompress(4, ip, in.size(), oout.data(), oout.size(), &olen);
