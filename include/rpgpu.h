@@ -211,10 +211,10 @@ typedef struct rpgpu_opts {
      * gzip batches (an LZ4 or snappy topic) sets a small value (minimum 256):
      * its zstd / gzip batches still decode, each lane taking more of them. */
     uint32_t decomp_ws_lanes;
-    /* RPGPU_OPT_WALK_OVERLAP: 0 or 1 = checksums and record walks side by
-     * side over the whole arena (one launch each); k > 1 = the arena
-     * checksummed in k chunks, each chunk's walk beside the next chunk's
-     * checksums (at most 256). */
+    /* RPGPU_OPT_WALK_OVERLAP: k > 1 = the arena checksummed in k chunks, each
+     * chunk's walk beside the next chunk's checksums (0 = 16; at most 256);
+     * 1 = checksums and speculative record walks side by side over the whole
+     * arena, one launch each (slower on C2: 4.97 vs 4.26 ms per step). */
     uint16_t walk_chunks;
     /* validate_kernel workgroups per CU of the persistent grid (0 = 8,
      * capped by occupancy; 5 beside a side-by-side walk; at most 32). */

@@ -222,9 +222,10 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
         delete c;
         return nullptr;
     }
-    // RPGPU_OPT_WALK_OVERLAP: checksums and walks side by side (1, the default)
-    // or chunked (walk_chunks > 1; C2 16 chunks: 4.29-4.42 ms per step, round 3)
-    c->overlap.chunks = 1;
+    // RPGPU_OPT_WALK_OVERLAP: chunked (the default, 16 chunks) or checksums and
+    // walks side by side (walk_chunks 1): C2 4.26 vs 4.97 / 4.50 ms per step
+    // (5 / 6 checksum workgroups per CU, profiles/r4/NOTES.md r4b)
+    c->overlap.chunks = 16;
     if (opts && opts->walk_chunks >= 1 && opts->walk_chunks <= rpgpu::kMaxRunChunks) c->overlap.chunks = opts->walk_chunks;
     // side by side, the checksum grid leaves each SIMD room for a walk wave
     c->overlap.grid = c->cu_count * (opts && opts->blocks_per_cu ? (int)opts->blocks_per_cu : rpgpu::kSideBlocksPerCU);
