@@ -463,12 +463,16 @@ def main() -> int:
         dh = {abi.VERDICT_NAMES.get(int(v), str(int(v))): int(c)
               for v, c in zip(*np.unique(dres["verdict"], return_counts=True))}
         out["decompress_verdicts_rank0"] = dh
+    # PMC traffic of this exact workload (config, payload and batch count), if
+    # measured: profiles/traffic.json, scripts/traffic_sum.py
     prof = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(prof):
         try:
-            tr = json.load(open(prof)).get(args.config)
-            if tr and tr.get("batches") == n:
+            key = args.config if (not decompress or args.payload == "text") else f"{args.config}:{args.payload}"
+            tr = json.load(open(prof)).get(key)
+            if tr and tr.get("batches") == n and tr.get("payload", "text") == (args.payload if decompress else "text"):
                 out["roofline"]["traffic"] = tr.get("hbm_bytes_per_launch")
+                out["roofline"]["traffic_source"] = f"profiles/traffic.json[{key!r}]"
         except (OSError, ValueError):
             pass
 

@@ -6,7 +6,9 @@ the one timed step, merged into profiles/traffic.json under the config.
 FETCH_SIZE is reported raw: the decoders' reads are scattered 16-byte
 accesses, for which MI355X_MICROARCH.md's 2x streaming-read correction is
 uncalibrated; validate_kernel's streaming reads are doubled as the guide
-prescribes.  usage: traffic_sum.py <pmc dir> <config> <batches>"""
+prescribes.  usage: traffic_sum.py <pmc dir> <config> <batches> [payload]
+The entry is keyed by config and payload ("c3", "c3:alnum"), as bench.py
+looks it up."""
 import csv
 import glob
 import json
@@ -15,6 +17,8 @@ import sys
 from collections import defaultdict
 
 root, cfg, nb = sys.argv[1], sys.argv[2], int(sys.argv[3])
+payload = sys.argv[4] if len(sys.argv) > 4 else "text"
+key = cfg if payload == "text" else f"{cfg}:{payload}"
 # mean per dispatch of each kernel, times its launches per pipeline step (the
 # validation and the walk run twice: over the compressed and the rewritten
 # batches; the run may hold extra dispatches outside the step)
@@ -41,7 +45,7 @@ for c in tot:
         per[c][name] = v / len(disp[c][name]) * calls
 fetch = sum(v * (2.0 if "validate_kernel" in k else 1.0) for k, v in per["FETCH_SIZE"].items()) * 1024
 write = sum(per["WRITE_SIZE"].values()) * 1024
-out = {"batches": nb,
+out = {"batches": nb, "payload": payload,
        "kernel": ("validate_kernel + walk_kernel of one step (all chunk dispatches)" if plain
                   else "every rpgpu:: kernel of one pipeline step"),
        "fetch_bytes": int(fetch), "write_bytes": int(write),
@@ -52,7 +56,7 @@ out = {"batches": nb,
                  "(16-B/lane streaming reads, MI355X_MICROARCH.md); the decoders' scattered reads raw"}
 p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic.json")
 doc = json.load(open(p)) if os.path.exists(p) else {}
-doc[cfg] = out
+doc[key] = out
 json.dump(doc, open(p, "w"), indent=1)
 sums = {c: sum(v.values()) for c, v in per.items()}
-print(cfg, "fetch GB", round(fetch / 1e9, 2), "write GB", round(write / 1e9, 2), {k: f"{v:.3g}" for k, v in sums.items()})
+print(key, "fetch GB", round(fetch / 1e9, 2), "write GB", round(write / 1e9, 2), {k: f"{v:.3g}" for k, v in sums.items()})
