@@ -263,6 +263,11 @@ int32_t rpgpu_submit(rpgpu_ctx* ctx, const rpgpu_batch_desc* descs, uint32_t n,
 int32_t rpgpu_poll(rpgpu_ctx* ctx, rpgpu_ticket ticket);
 /* Blocks until the ticket completes. */
 int32_t rpgpu_wait(rpgpu_ctx* ctx, rpgpu_ticket ticket);
+/* Blocks until every *_device call issued on the context's own stream
+ * (hip_stream == NULL) has completed: the C caller's join point for device
+ * calls when it does not drive HIP streams itself.  A reactor thread must not
+ * call it (use rpgpu_submit + rpgpu_eventfd there). */
+int32_t rpgpu_sync(rpgpu_ctx* ctx);
 /* A non-blocking eventfd (EFD_NONBLOCK | EFD_CLOEXEC) owned by the context:
  * it becomes readable whenever a stage of a submission completes, so a
  * Seastar reactor awaits it with a readable() future on the fd (the

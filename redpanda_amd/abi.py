@@ -219,6 +219,7 @@ def lib() -> C.CDLL:
              C.POINTER(_u64), C.POINTER(_u64))
         _sig(L.rpgpu_poll, _i32, _vp, _u64)
         _sig(L.rpgpu_wait, _i32, _vp, _u64)
+        _sig(L.rpgpu_sync, _i32, _vp)
         _sig(L.rpgpu_validate_scratch_bytes, C.c_size_t, _u32)
         _sig(L.rpgpu_validate_device, _i32, _vp, _vp, _u32, _vp, _vp, _vp, _u64, _vp, _vp, _vp)
         _sig(L.rpgpu_plan_device, _i32, _vp, _vp, _u32, _vp, _vp, _vp, _vp)
@@ -282,7 +283,7 @@ def gen() -> C.CDLL:
 # every symbol include/rpgpu.h declares (checked by tests/test_abi.py)
 EXPORTED = [
     "rpgpu_abi_version", "rpgpu_open", "rpgpu_close", "rpgpu_last_error", "rpgpu_device_info",
-    "rpgpu_arena_alloc", "rpgpu_arena_free", "rpgpu_submit", "rpgpu_poll", "rpgpu_wait",
+    "rpgpu_arena_alloc", "rpgpu_arena_free", "rpgpu_submit", "rpgpu_poll", "rpgpu_wait", "rpgpu_sync",
     "rpgpu_eventfd", "rpgpu_kafka_error_code", "rpgpu_kafka_error_codes_device",
     "rpgpu_partition_summaries_device", "rpgpu_segment_parse_device", "rpgpu_remote_segment_parse_device",
     "rpgpu_compaction_scratch_bytes", "rpgpu_compaction_keep_device", "rpgpu_compaction_rewrite_scratch_bytes",

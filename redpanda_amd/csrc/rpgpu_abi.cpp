@@ -705,6 +705,13 @@ int32_t rpgpu_wait(rpgpu_ctx* c, rpgpu_ticket ticket) {
     return r;
 }
 
+int32_t rpgpu_sync(rpgpu_ctx* c) {
+    if (!c) return RPGPU_EINVAL;
+    (void)hipSetDevice(c->device);
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    return e == hipSuccess ? RPGPU_OK : fail(c, e, "stream synchronize");
+}
+
 // ---- synchronous scalar mirrors ------------------------------------------
 static int32_t crc_one(rpgpu_ctx* c, uint32_t seed, const void* p, size_t n, uint32_t* out) {
     (void)hipSetDevice(c->device);

@@ -9,7 +9,12 @@
  *        model/record_utils.cc:183-225, CRC32C bit by bit), submits them with
  *        rpgpu_submit, waits on rpgpu_eventfd with poll(2) and drains the
  *        ticket with rpgpu_poll -- the reactor-side pattern -- then checks
- *        verdicts, CRCs and index entries, and the scalar CRC mirrors.
+ *        verdicts, CRCs and index entries, and the scalar CRC mirrors; then
+ *        the device entry points a reader and the compactor call, on pinned
+ *        buffers (device-accessible) joined with rpgpu_sync: the tiered-storage
+ *        reader over an on-disk segment (rpgpu_remote_segment_parse_device,
+ *        remote_segment.cc:788-975) and the compaction rewrite of a batch
+ *        (rpgpu_compaction_rewrite_plan/run_device, compaction_reducers.cc:117-251).
  * Exit status 0 = every check passed; the failing check is printed. */
 #include <poll.h>
 #include <stdint.h>
@@ -88,6 +93,37 @@ static size_t make_batch(uint8_t* out, int64_t base_offset, int nrec, int vlen) 
     put_be(out + 57, (uint64_t)nrec, 4);
     put_be(out + 17, crc32c_bits(0, out + 21, total - 21), 4);
     return total;
+}
+
+static void put_le(uint8_t* o, uint64_t v, int nb) {
+    for (int i = 0; i < nb; i++) o[i] = (uint8_t)(v >> (8 * i));
+}
+static uint64_t get_be(const uint8_t* p, int nb) {
+    uint64_t v = 0;
+    for (int i = 0; i < nb; i++) v = (v << 8) | p[i];
+    return v;
+}
+
+/* the on-disk form of a wire batch (storage/parser.cc:40-80): little-endian
+ * header with the batch type and header_crc, the same Kafka crc and body */
+static size_t make_disk_batch(uint8_t* out, int64_t base_offset, int nrec, int vlen, int8_t type) {
+    uint8_t wire[8192];
+    const size_t n = make_batch(wire, base_offset, nrec, vlen);
+    memcpy(out + 61, wire + 61, n - 61);
+    put_le(out + 4, n, 4);
+    put_le(out + 8, get_be(wire + 0, 8), 8);
+    out[16] = (uint8_t)type;
+    put_le(out + 17, get_be(wire + 17, 4), 4);
+    put_le(out + 21, get_be(wire + 21, 2), 2);
+    put_le(out + 23, get_be(wire + 23, 4), 4);
+    put_le(out + 27, get_be(wire + 27, 8), 8);
+    put_le(out + 35, get_be(wire + 35, 8), 8);
+    put_le(out + 43, get_be(wire + 43, 8), 8);
+    put_le(out + 51, get_be(wire + 51, 2), 2);
+    put_le(out + 53, get_be(wire + 53, 4), 4);
+    put_le(out + 57, get_be(wire + 57, 4), 4);
+    put_le(out + 0, crc32c_bits(0, out + 4, 57), 4); /* internal_header_only_crc */
+    return n;
 }
 
 static int run_cpu(void) {
@@ -194,6 +230,77 @@ static int run_gpu(void) {
     uint32_t hc = 0;
     CHECK(rpgpu_internal_header_only_crc(ctx, &h, &hc) == RPGPU_OK);
     CHECK(hc == crc32c_bits(0, (const uint8_t*)&h + 4, 57));
+
+    /* ---- tiered-storage reader: raft_data, raft_configuration, raft_data */
+    uint8_t* pin = (uint8_t*)rpgpu_arena_alloc(ctx, 1 << 20);
+    CHECK(pin != NULL);
+    if (pin) {
+        uint8_t* seg = pin;
+        size_t sl = 0;
+        sl += make_disk_batch(seg + sl, 0, 5, 80, 1);
+        sl += make_disk_batch(seg + sl, 5, 1, 20, 2); /* configuration: an offset-translation gap */
+        sl += make_disk_batch(seg + sl, 6, 3, 60, 1);
+        rpgpu_remote_read* rd = (rpgpu_remote_read*)(pin + 65536);
+        memset(rd, 0, sizeof(*rd));
+        rd->offset = 0;
+        rd->length = sl;
+        rd->desc_cap = 4;
+        rd->gap_cap = 4;
+        rd->ops = RPGPU_OPS_PRODUCE;
+        rd->max_offset = INT64_MAX;
+        rd->max_bytes = UINT64_MAX;
+        rpgpu_remote_parse_result* rr = (rpgpu_remote_parse_result*)(pin + 65536 + 256);
+        rpgpu_batch_desc* rdesc = (rpgpu_batch_desc*)(pin + 65536 + 512);
+        int64_t* kbase = (int64_t*)(pin + 65536 + 1024);
+        int64_t* gaps = (int64_t*)(pin + 65536 + 1536);
+        CHECK(rpgpu_remote_segment_parse_device(ctx, seg, rd, 1, rr, rdesc, kbase, gaps, NULL) == RPGPU_OK);
+        CHECK(rpgpu_sync(ctx) == RPGPU_OK);
+        CHECK(rr->status == RPGPU_V_OK);
+        CHECK(rr->accepted == 2 && rr->gaps == 1 && rr->cur_delta == 1);
+        CHECK(kbase[0] == 0 && kbase[1] == 5); /* rp_to_kafka: 6 - delta 1 */
+        CHECK(gaps[0] == 5 && gaps[1] == 5);
+        CHECK(rdesc[0].offset == 0 && rdesc[1].format == RPGPU_FMT_RP_DISK);
+
+        /* ---- compaction rewrite of batch 0 of the first submission: keep records 0, 2, 4 */
+        uint8_t* data = pin + 131072;
+        memcpy(data, arena, off);
+        rpgpu_batch_desc* cd = (rpgpu_batch_desc*)(pin + 262144);
+        memcpy(cd, d, sizeof(d[0]));
+        rpgpu_batch_result* cres_in = (rpgpu_batch_result*)(pin + 262144 + 256);
+        memcpy(cres_in, res, sizeof(res[0]));
+        rpgpu_record_index* cidx = (rpgpu_record_index*)(pin + 262144 + 512);
+        memcpy(cidx, idx, 5 * sizeof(idx[0]));
+        uint8_t* keep = pin + 262144 + 1024;
+        const uint8_t k5[5] = {1, 0, 1, 0, 1};
+        memcpy(keep, k5, 5);
+        uint64_t* obytes = (uint64_t*)(pin + 262144 + 1088);
+        uint8_t* scratch = pin + 327680;
+        CHECK(rpgpu_compaction_rewrite_scratch_bytes(1) <= 65536);
+        CHECK(rpgpu_compaction_rewrite_plan_device(ctx, data, cd, cres_in, 1, cidx, 5, keep, obytes, scratch, NULL) ==
+              RPGPU_OK);
+        CHECK(rpgpu_sync(ctx) == RPGPU_OK);
+        CHECK(*obytes > 61 && *obytes < 65536);
+        rpgpu_compact_result* cr = (rpgpu_compact_result*)(pin + 393216);
+        uint8_t* cout = pin + 458752;
+        rpgpu_batch_desc* odesc = (rpgpu_batch_desc*)(pin + 393216 + 256);
+        rpgpu_batch_result* ores = (rpgpu_batch_result*)(pin + 393216 + 512);
+        rpgpu_record_index* oidx = (rpgpu_record_index*)(pin + 393216 + 1024);
+        uint64_t* oused = (uint64_t*)(pin + 393216 + 2048);
+        CHECK(rpgpu_compaction_rewrite_run_device(ctx, data, cd, cres_in, 1, cidx, 5, keep, cr, cout,
+                                                  *obytes + RPGPU_ARENA_TAIL_PAD, odesc, ores, oidx, 8, oused,
+                                                  scratch, NULL) == RPGPU_OK);
+        CHECK(rpgpu_sync(ctx) == RPGPU_OK);
+        CHECK(cr->action == RPGPU_COMPACT_FILTERED && cr->record_count == 3 && cr->removed == 2);
+        CHECK(ores->verdict == RPGPU_V_OK && ores->record_count == 3 && ores->index_count == 3);
+        CHECK(oidx[0].offset == 0 && oidx[1].offset == 2 && oidx[2].offset == 4);
+        /* the rewritten batch carries fresh CRCs (reset_size_checksum_metadata) */
+        CHECK(ores->crc == ores->crc_expected);
+        const uint8_t* ob = cout + cr->out_offset;
+        const uint32_t stored = (uint32_t)ob[0] | ((uint32_t)ob[1] << 8) | ((uint32_t)ob[2] << 16) |
+                                ((uint32_t)ob[3] << 24);
+        CHECK(stored == crc32c_bits(0, ob + 4, 57) && ores->header_crc == stored);
+        rpgpu_arena_free(ctx, pin);
+    }
     rpgpu_arena_free(ctx, arena);
     rpgpu_close(ctx);
     return 0;
