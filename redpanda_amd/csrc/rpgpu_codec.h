@@ -558,6 +558,47 @@ RPC_HD uint32_t w64_dword(const Win64 W, uint32_t q) {  // by value: keeps W out
     const uint32_t c0 = (q & 4) ? b1 : b0, c1 = (q & 4) ? b3 : b2;
     return q >= 16 ? 0u : ((q & 8) ? c1 : c0);
 }
+// window bytes [o, o + 16) for 0 <= o <= 48: a four-stage select network
+// picks dwords q .. q + 4 (q = o / 4), then a byte align -- ~35 VALU, no load
+#ifndef RPGPU_LZ4_WINLIT
+#define RPGPU_LZ4_WINLIT 1  // literals of short runs taken from the window, not reloaded
+#endif
+RPC_HD V16 w64_get16(const Win64 W, uint32_t o) {
+    const uint32_t q = o >> 2;
+    const bool b3 = q & 8, b2 = q & 4, b1 = q & 2, b0 = q & 1;
+    // stage 3: t[i] = w[i + 8 * b3], i < 12 (dwords past 15 read as zero)
+    const uint32_t t0 = b3 ? W.w8 : W.w0, t1 = b3 ? W.w9 : W.w1, t2 = b3 ? W.w10 : W.w2, t3 = b3 ? W.w11 : W.w3;
+    const uint32_t t4 = b3 ? W.w12 : W.w4, t5 = b3 ? W.w13 : W.w5, t6 = b3 ? W.w14 : W.w6, t7 = b3 ? W.w15 : W.w7;
+    const uint32_t t8 = b3 ? 0u : W.w8, t9 = b3 ? 0u : W.w9, t10 = b3 ? 0u : W.w10, t11 = b3 ? 0u : W.w11;
+    // stage 2: u[i] = t[i + 4 * b2], i < 8
+    const uint32_t u0 = b2 ? t4 : t0, u1 = b2 ? t5 : t1, u2 = b2 ? t6 : t2, u3 = b2 ? t7 : t3;
+    const uint32_t u4 = b2 ? t8 : t4, u5 = b2 ? t9 : t5, u6 = b2 ? t10 : t6, u7 = b2 ? t11 : t7;
+    // stage 1: v[i] = u[i + 2 * b1], i < 6; stage 0: x[i] = v[i + b0], i < 5
+    const uint32_t v0 = b1 ? u2 : u0, v1 = b1 ? u3 : u1, v2 = b1 ? u4 : u2, v3 = b1 ? u5 : u3, v4 = b1 ? u6 : u4,
+                   v5 = b1 ? u7 : u5;
+    const uint32_t x0 = b0 ? v1 : v0, x1 = b0 ? v2 : v1, x2 = b0 ? v3 : v2, x3 = b0 ? v4 : v3, x4 = b0 ? v5 : v4;
+    const uint32_t s = o & 3u;
+#ifdef __HIPCC__
+    const uint32_t y0 = __builtin_amdgcn_alignbyte(x1, x0, s), y1 = __builtin_amdgcn_alignbyte(x2, x1, s);
+    const uint32_t y2 = __builtin_amdgcn_alignbyte(x3, x2, s), y3 = __builtin_amdgcn_alignbyte(x4, x3, s);
+#else
+    auto ab = [](uint32_t hi, uint32_t lo, uint32_t k) {
+        return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * k));
+    };
+    const uint32_t y0 = ab(x1, x0, s), y1 = ab(x2, x1, s), y2 = ab(x3, x2, s), y3 = ab(x4, x3, s);
+#endif
+    return V16{((uint64_t)y1 << 32) | y0, ((uint64_t)y3 << 32) | y2};
+}
+// 16 literal bytes at input offset p: from the window when they lie inside
+// it, else a load
+RPC_HD V16 lit16(const Win64& W, const uint8_t* in, int32_t p) {
+#if RPGPU_LZ4_WINLIT
+    const int32_t o = p - W.pos;
+    if (o >= 0 && o <= 48) return w64_get16(W, (uint32_t)o);
+#endif
+    return v16_ld(in + p);
+}
+
 // 4 input bytes from p (little-endian), [p, p + need) inside the window
 // (reloaded there if not: a dependent load, off the common path)
 RPC_HD uint32_t w64_at(Win64& W, const uint8_t* in, int32_t p, int32_t need, int32_t lim) {
@@ -709,8 +750,8 @@ int32_t lz4_block_lane(const uint8_t* in, int32_t isz, uint8_t* out, int32_t oca
         const int32_t rel = ll - off;  // match source start - literal start
         const uint8_t* src = out + op_m - off;
         V16 L0{0, 0}, L1{0, 0}, A0{0, 0}, A1{0, 0};
-        if (ll > 0) L0 = v16_ld(in + ip_lit);
-        if (ll > 16) L1 = v16_ld(in + ip_lit + 16);
+        if (ll > 0) L0 = lit16(W, in, ip_lit);
+        if (ll > 16) L1 = lit16(W, in, ip_lit + 16);
         if (off != 0 && rel < 0) A0 = v16_ld(src);
         if (!pat && nch > 1 && rel + 16 < 0) A1 = v16_ld(src + 16);
 #if RPGPU_LZ4_WC
