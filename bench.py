@@ -254,6 +254,8 @@ def main() -> int:
     ap.add_argument("--payload", default="text", choices=["text", "alnum"],
                     help="record payload of the compressed configs (text: Zipf words, alnum: random)")
     ap.add_argument("--walk-chunks", type=int, default=0, help="rpgpu_opts.walk_chunks (tuning; 0 = default)")
+    ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
+                    help="RPGPU_OPT_WALK_OVERLAP (auto: on for the uncompressed configs)")
     ap.add_argument("--blocks-per-cu", type=int, default=0, help="rpgpu_opts.blocks_per_cu (tuning; 0 = default)")
     args = ap.parse_args()
 
@@ -282,7 +284,8 @@ def main() -> int:
     if args.ops:
         spec.ops = args.ops
     # chunked checksum / walk overlap for the uniform uncompressed arenas (RPGPU_OPT_WALK_OVERLAP)
-    eng = engine.Engine(local, walk_overlap=not decompress, decomp_ws_lanes=cfg.get("ws_lanes", 0),
+    overlap = (not decompress) if args.overlap == "auto" else args.overlap == "on"
+    eng = engine.Engine(local, walk_overlap=overlap, decomp_ws_lanes=cfg.get("ws_lanes", 0),
                         walk_chunks=args.walk_chunks, blocks_per_cu=args.blocks_per_cu)
     chunks, P_total, part_shift, (plo, phi) = rank_chunks(cfg, rank, world, scaling, args.batches)
     n = sum(m for _, m in chunks)

@@ -510,7 +510,8 @@ __global__ __launch_bounds__(256) void walk_kernel(const rpgpu_batch_desc* __res
                                                    rpgpu_record_index* __restrict__ index,
                                                    const uint32_t* __restrict__ local_first,
                                                    const uint32_t* __restrict__ caps,
-                                                   const uint64_t* __restrict__ block_base, uint64_t index_cap) {
+                                                   const uint64_t* __restrict__ block_base, uint64_t index_cap,
+                                                   uint32_t* __restrict__ wave_list, uint32_t* __restrict__ wave_count) {
     const uint32_t b = b0 + blockIdx.x * blockDim.x + threadIdx.x;
     WalkJob J;
     J.flags = 0;
@@ -535,9 +536,59 @@ __global__ __launch_bounds__(256) void walk_kernel(const rpgpu_batch_desc* __res
             J.cap = (uint32_t)cap;
             J.b = b;
             J.flags = kJobLive | ((d.ops & RPGPU_OP_INDEX) ? kJobIndex : 0u);
+            if (J.rc > kWaveWalkMin) {  // many records: walk_wave_kernel's
+                wave_list[atomicAdd(wave_count, 1u)] = b;
+                J.flags = 0;
+            }
         }
     }
     walk_lanes(data, J, index, res);
+}
+
+// The batches walk_kernel listed (more than kWaveWalkMin records): one
+// wavefront each, taken from an atomic queue (rpgpu_walk.h wave_walk_batch).
+__global__ __launch_bounds__(256) void walk_wave_kernel(const rpgpu_batch_desc* __restrict__ descs,
+                                                        const uint8_t* __restrict__ data,
+                                                        rpgpu_batch_result* __restrict__ res,
+                                                        rpgpu_record_index* __restrict__ index,
+                                                        const uint32_t* __restrict__ local_first,
+                                                        const uint32_t* __restrict__ caps,
+                                                        const uint64_t* __restrict__ block_base, uint64_t index_cap,
+                                                        const uint32_t* __restrict__ wave_list,
+                                                        const uint32_t* __restrict__ wave_count,
+                                                        uint32_t* __restrict__ head) {
+    const uint32_t cnt = *wave_count;
+    for (;;) {
+        uint32_t k = 0;
+        if (lane_id() == 0) k = atomicAdd(head, 1u);
+        k = __builtin_amdgcn_readfirstlane(k);
+        if (k >= cnt) break;
+        const uint32_t b = wave_list[k];
+        const rpgpu_batch_desc d = descs[b];
+        const rpgpu_batch_result& r = res[b];
+        const uint64_t first = block_base[b / kScanBlock] + local_first[b];
+        uint64_t cap = caps[b];
+        if (first >= index_cap) cap = 0;
+        else if (first + cap > index_cap) cap = index_cap - first;
+        WalkJob J;
+        J.body = d.offset + kHeaderSize;
+        J.base_offset = r.base_offset;
+        J.first_ts = r.first_timestamp;
+        J.n = (uint32_t)r.size_bytes - kHeaderSize;
+        J.rc = r.record_count;
+        J.first = (uint32_t)first;
+        J.cap = (uint32_t)cap;
+        J.b = b;
+        J.flags = kJobLive | ((d.ops & RPGPU_OP_INDEX) ? kJobIndex : 0u);
+        int32_t verdict;
+        uint32_t count;
+        wave_walk_batch(data, J, index, verdict, count);
+        if (lane_id() == 0) {
+            uint32_t* o = reinterpret_cast<uint32_t*>(res + b);
+            o[0] = (uint32_t)verdict;
+            o[15] = count;
+        }
+    }
 }
 
 // The walk side of the concurrent checksum / walk (rpgpu_walk.h): one lane
@@ -1175,16 +1226,25 @@ hipError_t launch_kafka_codes(const rpgpu_batch_result* d_res, uint32_t n, uint3
 }
 
 // ------------------------------------------------------------ launchers
-// scratch layout: caps[n] u32 | local_first[n] u32 | block_sum[nb] u64 | side[n] u64
+// scratch layout: caps[n] u32 | local_first[n] u32 | block_sum[nb] u64 |
+//                 side[n] u64 | wave counters (count, head; 64 B) | wave_list[n] u32
+struct WaveWalk {
+    uint32_t *list, *count;  // count[0]: batches listed, count[1]: queue head
+};
 static void scratch_parts(void* d_scratch, uint32_t n, uint32_t** caps, uint32_t** local_first,
-                          uint64_t** block_sum, uint64_t** side = nullptr) {
+                          uint64_t** block_sum, uint64_t** side = nullptr, WaveWalk* ww = nullptr) {
     uint8_t* sc = static_cast<uint8_t*>(d_scratch);
     *caps = reinterpret_cast<uint32_t*>(sc);
     *local_first = *caps + n;
     const size_t o_bs = ((size_t)n * 8 + 15) & ~(size_t)15;
     *block_sum = reinterpret_cast<uint64_t*>(sc + o_bs);
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
-    if (side) *side = reinterpret_cast<uint64_t*>(sc + ((o_bs + nb * 8 + 63) & ~(size_t)63));
+    const size_t o_side = (o_bs + nb * 8 + 63) & ~(size_t)63;
+    if (side) *side = reinterpret_cast<uint64_t*>(sc + o_side);
+    if (ww) {
+        ww->count = reinterpret_cast<uint32_t*>(sc + o_side + (size_t)n * 8);
+        ww->list = ww->count + 16;
+    }
 }
 
 hipError_t launch_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
@@ -1222,7 +1282,8 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
     if (n == 0) return hipSuccess;
     uint32_t *caps, *local_first;
     uint64_t *block_sum, *side;
-    scratch_parts(const_cast<void*>(d_scratch), n, &caps, &local_first, &block_sum, &side);
+    WaveWalk ww;
+    scratch_parts(const_cast<void*>(d_scratch), n, &caps, &local_first, &block_sum, &side, &ww);
     hipError_t e = hipSuccess;
     if (ov && n >= kRunChunkMin && ov->chunks == 1) {
         if ((e = hipEventRecord(ov->ev[0], s)) != hipSuccess) return e;
@@ -1242,6 +1303,8 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
         return hipGetLastError();
     }
     const uint32_t chunks = (ov && n >= kRunChunkMin) ? (uint32_t)ov->chunks : 1u;
+    if ((e = hipMemsetAsync(ww.count, 0, 2 * sizeof(uint32_t), s)) != hipSuccess) return e;
+    hipStream_t ws = s;  // the walks' stream
     for (uint32_t k = 0; k < chunks; k++) {
         const uint32_t lo = (uint32_t)((uint64_t)n * k / chunks), hi = (uint32_t)((uint64_t)n * (k + 1) / chunks);
         const uint32_t need = (hi - lo + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -1249,14 +1312,20 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
         validate_kernel<<<g, kValidateThreads, 0, s>>>(d_descs, lo, hi, d_data, d_res, d_index, local_first, caps,
                                                         block_sum, index_cap, d_tables);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        hipStream_t ws = s;
         if (chunks > 1) {
             if ((e = hipEventRecord(ov->ev[k], s)) != hipSuccess) return e;
             if ((e = hipStreamWaitEvent(ov->aux, ov->ev[k], 0)) != hipSuccess) return e;
             ws = ov->aux;
         }
         walk_kernel<<<(hi - lo + 255) / 256, 256, 0, ws>>>(d_descs, lo, hi, d_data, d_res, d_index, local_first,
-                                                           caps, block_sum, index_cap);
+                                                           caps, block_sum, index_cap, ww.list, ww.count);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    // batches of many records, a wavefront each, after the lane walks
+    {
+        const uint32_t wg = (n < 2048u ? (n + 3) / 4 : 512u);
+        walk_wave_kernel<<<wg, 256, 0, ws>>>(d_descs, d_data, d_res, d_index, local_first, caps, block_sum, index_cap,
+                                             ww.list, ww.count, ww.count + 1);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (chunks > 1) {  // the caller's stream sees the last walk
@@ -1291,7 +1360,8 @@ hipError_t validate_occupancy(int* blocks_per_cu) {
 
 size_t validate_scratch_bytes(uint32_t n) {
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
-    return (((((size_t)n * 8 + 15) & ~(size_t)15) + nb * 8 + 63) & ~(size_t)63) + (size_t)n * 8 + 64;
+    return (((((size_t)n * 8 + 15) & ~(size_t)15) + nb * 8 + 63) & ~(size_t)63) + (size_t)n * 8 + 64 +
+           (size_t)n * 4 + 64;
 }
 
 }  // namespace rpgpu

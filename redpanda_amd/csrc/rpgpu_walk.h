@@ -127,6 +127,45 @@ __device__ __forceinline__ void store_entry(rpgpu_record_index* e, int64_t off, 
     dst[1] = b;
 }
 
+// One record of parse_one_record_copy_from_buffer (record_utils.cc:116-176)
+// from body offset pos: RPGPU_V_OK with its fields and pos past it, or the
+// verdict the record fails with.
+struct Rec {
+    int64_t ts_delta, off_delta, klen, vlen, key_off, val_off;
+};
+__device__ __forceinline__ int32_t walk_record(Window& W, const uint8_t* body, int64_t n, int64_t& pos, Rec& r) {
+    (void)read_varlong(W, body, n, pos);  // record size: not used by the parse
+    if (pos >= n) return RPGPU_V_REC_ATTR_EOF;  // consume_type<int8_t> throws
+    pos += 1;                                  // attributes
+    r.ts_delta = read_varlong(W, body, n, pos);
+    r.off_delta = read_varlong(W, body, n, pos);
+    r.klen = read_varlong(W, body, n, pos);
+    r.key_off = pos;
+    if (r.klen > 0 && !parser_copy(n, pos, r.klen)) return RPGPU_V_REC_UNDEFINED;
+    r.vlen = read_varlong(W, body, n, pos);
+    r.val_off = pos;
+    if (r.vlen > 0 && !parser_copy(n, pos, r.vlen)) return RPGPU_V_REC_UNDEFINED;
+    // parse_record_headers (record_utils.cc:93-114)
+    const int64_t hcount = read_varlong(W, body, n, pos);
+    if (hcount < 0) return RPGPU_V_REC_HCOUNT_NEG;  // reserve(size_t(negative)) -> length_error
+    if (hcount > kHcountLimit) return RPGPU_V_REC_UNDEFINED;
+    for (int64_t h = 0; h < hcount; h++) {
+        if (pos >= n) break;  // every further header is a no-op at end of input
+        const int64_t hk = read_varlong(W, body, n, pos);
+        if (hk > 0 && !parser_copy(n, pos, hk)) return RPGPU_V_REC_UNDEFINED;
+        const int64_t hv = read_varlong(W, body, n, pos);
+        if (hv > 0 && !parser_copy(n, pos, hv)) return RPGPU_V_REC_UNDEFINED;
+    }
+    return RPGPU_V_OK;
+}
+__device__ __forceinline__ void entry_of(const WalkJob& J, const Rec& r, u32x4& a, u32x4& e) {
+    const uint64_t off = J.base_offset + (uint64_t)(int64_t)(int32_t)r.off_delta;
+    const uint64_t ts = (uint64_t)J.first_ts + (uint64_t)r.ts_delta;
+    a = (u32x4){(uint32_t)off, (uint32_t)(off >> 32), (uint32_t)ts, (uint32_t)(ts >> 32)};
+    e = (u32x4){(uint32_t)(r.key_off + kHeaderSize), (uint32_t)r.klen, (uint32_t)(r.val_off + kHeaderSize),
+                (uint32_t)r.vlen};
+}
+
 // Walks lane j's batch: its record verdict and the index entries written
 // (min(records, cap); 0 without kJobIndex).
 __device__ __forceinline__ void walk_batch(const uint8_t* __restrict__ data, WalkJob J,
@@ -152,66 +191,16 @@ __device__ __forceinline__ void walk_batch(const uint8_t* __restrict__ data, Wal
             live = false;
             continue;
         }
-        (void)read_varlong(W, body, n, pos);  // record size: not used by the parse
-        if (pos >= n) {                       // consume_type<int8_t> throws
-            verdict = RPGPU_V_REC_ATTR_EOF;
-            live = false;
-            continue;
-        }
-        pos += 1;  // attributes
-        const int64_t ts_delta = read_varlong(W, body, n, pos);
-        const int64_t off_delta = read_varlong(W, body, n, pos);
-        const int64_t klen = read_varlong(W, body, n, pos);
-        const int64_t key_off = pos;
-        if (klen > 0 && !parser_copy(n, pos, klen)) {
-            verdict = RPGPU_V_REC_UNDEFINED;
-            live = false;
-            continue;
-        }
-        const int64_t vlen = read_varlong(W, body, n, pos);
-        const int64_t val_off = pos;
-        if (vlen > 0 && !parser_copy(n, pos, vlen)) {
-            verdict = RPGPU_V_REC_UNDEFINED;
-            live = false;
-            continue;
-        }
-        // parse_record_headers (record_utils.cc:93-114)
-        const int64_t hcount = read_varlong(W, body, n, pos);
-        if (hcount < 0) {  // reserve(size_t(negative)) -> length_error
-            verdict = RPGPU_V_REC_HCOUNT_NEG;
-            live = false;
-            continue;
-        }
-        if (hcount > kHcountLimit) {
-            verdict = RPGPU_V_REC_UNDEFINED;
-            live = false;
-            continue;
-        }
-        bool bad = false;
-        for (int64_t h = 0; h < hcount; h++) {
-            if (pos >= n) break;  // every further header is a no-op at end of input
-            const int64_t hk = read_varlong(W, body, n, pos);
-            if (hk > 0 && !parser_copy(n, pos, hk)) {
-                bad = true;
-                break;
-            }
-            const int64_t hv = read_varlong(W, body, n, pos);
-            if (hv > 0 && !parser_copy(n, pos, hv)) {
-                bad = true;
-                break;
-            }
-        }
-        if (bad) {
-            verdict = RPGPU_V_REC_UNDEFINED;
+        Rec r;
+        const int32_t v = walk_record(W, body, n, pos, r);
+        if (v != RPGPU_V_OK) {
+            verdict = v;
             live = false;
             continue;
         }
         if ((J.flags & kJobIndex) && cnt < J.cap) {
-            const uint64_t off = J.base_offset + (uint64_t)(int64_t)(int32_t)off_delta;
-            const uint64_t ts = (uint64_t)J.first_ts + (uint64_t)ts_delta;
-            const u32x4 a = {(uint32_t)off, (uint32_t)(off >> 32), (uint32_t)ts, (uint32_t)(ts >> 32)};
-            const u32x4 e = {(uint32_t)(key_off + kHeaderSize), (uint32_t)klen, (uint32_t)(val_off + kHeaderSize),
-                             (uint32_t)vlen};
+            u32x4 a, e;
+            entry_of(J, r, a, e);
             // entries leave in aligned pairs (64 bytes): an even slot waits for
             // its odd neighbour (32-byte stores to scattered half-lines were
             // written back at 2.4x, profiles/r3/pmc_c2)
@@ -241,6 +230,134 @@ __device__ __forceinline__ void walk_batch(const uint8_t* __restrict__ data, Wal
     }
     verdict_out = verdict;
     count_out = (J.flags & kJobIndex) ? (cnt < J.cap ? cnt : J.cap) : 0u;
+}
+
+// ---- wave walk: batches of many records (walk_wave_kernel) -----------------
+// A lane walks its batch one record at a time, each record a dependent window
+// read: a 1 MiB batch of 17-byte records is ~60,000 of them in a row.  Above
+// kWaveWalkMin records a wavefront walks the batch instead:
+//   - the record starts, from the `length` varints (record_utils.cc:183-225
+//     writes the record's size first): a wave-uniform chain over a 1 KiB
+//     chunk of the body held in the wave's registers, 64 starts at a time;
+//   - each lane walks one record from its start exactly as walk_record does
+//     (the reference never navigates by the length, model/record.h:668-691)
+//     and the record counts only if its walk ends where the next start is;
+//   - a group's 64 entries are stored together once all of them check out.
+// Any disagreement (a negative or overlong length, a record that fails, a
+// field walk that does not end at the next start) hands the batch to the
+// serial walk (lane 0, walk_batch), so verdicts and entries are the walk's.
+constexpr int32_t kWaveWalkMin = 1024;
+
+// dword q of the 1 KiB chunk the wave holds (lane q / 4, component q % 4)
+__device__ __forceinline__ uint32_t chunk_dword(const u32x4& C, uint32_t q) {
+    const uint32_t c = q & 3u;
+    const uint32_t v = c == 0 ? C.x : c == 1 ? C.y : c == 2 ? C.z : C.w;
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(q >> 2));
+}
+// read_varlong over 12 bytes b0..b11 (x = bytes 0..7, d2 = 8..11) of which
+// `lim` (<= 10) may be read: the zigzag value, and the bytes consumed in nb
+__device__ __forceinline__ int64_t varlong12(uint64_t x, uint32_t d2, uint32_t lim, uint32_t& nb) {
+    uint64_t t8 = ~x & 0x8080808080808080ull;
+    uint32_t t2 = ~d2 & 0x8080u;
+    const uint32_t term = t8 ? ((uint32_t)__builtin_ctzll(t8) >> 3) : (t2 ? 8u + ((uint32_t)__builtin_ctz(t2) >> 3) : 10u);
+    nb = term < lim ? term + 1 : lim;
+    uint64_t y = x & 0x7f7f7f7f7f7f7f7full;
+    if (nb < 8) y &= (1ull << (8 * nb)) - 1;
+    y = (y & 0x007f007f007f007full) | ((y & 0x7f007f007f007f00ull) >> 1);
+    y = (y & 0x00003fff00003fffull) | ((y & 0x3fff00003fff0000ull) >> 2);
+    y = (y & 0x000000000fffffffull) | ((y & 0x0fffffff00000000ull) >> 4);
+    if (nb > 8) y |= (uint64_t)(d2 & 0x7fu) << 56;
+    if (nb > 9) y |= (uint64_t)((d2 >> 8) & 1u) << 63;
+    return (int64_t)((y >> 1) ^ (~(y & 1) + 1));
+}
+
+// J is wave-uniform (every lane holds the same job).
+__device__ __forceinline__ void wave_walk_batch(const uint8_t* __restrict__ data, WalkJob J,
+                                                rpgpu_record_index* __restrict__ index, int32_t& verdict_out,
+                                                uint32_t& count_out) {
+    const uint32_t l = lane_id();
+    const uint8_t* body = data + J.body;
+    const int64_t n = J.n;
+    const bool want_index = (J.flags & kJobIndex) != 0;
+    rpgpu_record_index* idx = index + J.first;
+    int64_t s = 0;        // next record start (the length chain)
+    int64_t i = 0;        // records verified
+    int64_t cb = -4096;   // body offset of the chunk in C
+    u32x4 C = {0, 0, 0, 0};
+    bool ok = true;
+    while (ok && i < (int64_t)J.rc) {
+        // ---- up to 64 starts, chained through the length varints
+        uint32_t vstart = 0, vnext = 0;
+        uint32_t g = 0;
+        while (g < 64 && i + g < (int64_t)J.rc) {
+            if (s >= n) {  // the chain ran off the body: the serial walk decides
+                ok = false;
+                break;
+            }
+            if (s < cb || s + 12 > cb + 1024) {
+                cb = s & ~(int64_t)15;
+                // lanes past the body's readable end (its 64-byte tail) load nothing
+                C = cb + 16 * (int64_t)l + 16 <= n + 64 ? ld16(body + cb + 16 * l) : (u32x4){0, 0, 0, 0};
+            }
+            const uint32_t o = (uint32_t)(s - cb), q = o >> 2, sh = 8 * (o & 3u);
+            const uint32_t w0 = chunk_dword(C, q), w1 = chunk_dword(C, q + 1), w2 = chunk_dword(C, q + 2),
+                           w3 = chunk_dword(C, q + 3);
+            const uint32_t b0 = sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
+            const uint32_t b1 = sh ? (w1 >> sh) | (w2 << (32 - sh)) : w1;
+            const uint32_t b2 = sh ? (w2 >> sh) | (w3 << (32 - sh)) : w2;
+            const int64_t avail = n - s;
+            uint32_t nb;
+            const int64_t len = varlong12(((uint64_t)b1 << 32) | b0, b2, avail < 10 ? (uint32_t)avail : 10u, nb);
+            if (len < 0 || len > n - s) {
+                ok = false;
+                break;
+            }
+            const int64_t next = s + nb + len;
+            vstart = l == g ? (uint32_t)s : vstart;
+            vnext = l == g ? (uint32_t)next : vnext;
+            s = next;
+            g++;
+        }
+        if (!ok) break;
+        // ---- each lane walks its record; the group counts if every walk ends
+        //      at the next start
+        bool good = true;
+        u32x4 a = {0, 0, 0, 0}, e = {0, 0, 0, 0};
+        if (l < g) {
+            Window W;
+            window_load(W, body, (int64_t)vstart);
+            int64_t pos = (int64_t)vstart;
+            Rec r;
+            const int32_t v = walk_record(W, body, n, pos, r);
+            good = v == RPGPU_V_OK && pos == (int64_t)vnext;
+            entry_of(J, r, a, e);
+        }
+        if (wave_any(!good)) {
+            ok = false;
+            break;
+        }
+        if (want_index && l < g && i + l < (int64_t)J.cap) {
+            u32x4* dst = reinterpret_cast<u32x4*>(idx + i + l);
+            dst[0] = a;
+            dst[1] = e;
+        }
+        i += g;
+    }
+    if (ok) {
+        // every record checked out; the walk ends at the last record's end
+        verdict_out = s < n ? RPGPU_V_REC_TRAILING : RPGPU_V_OK;
+        const int64_t rc = J.rc > 0 ? (int64_t)J.rc : 0;
+        count_out = want_index ? (uint32_t)(rc < (int64_t)J.cap ? rc : (int64_t)J.cap) : 0u;
+        return;
+    }
+    // the serial walk, in lane 0
+    WalkJob J0 = J;
+    if (l != 0) J0.flags = 0;
+    int32_t v;
+    uint32_t c;
+    walk_batch(data, J0, index, v, c);
+    verdict_out = (int32_t)__builtin_amdgcn_readfirstlane(v);
+    count_out = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
 }
 
 // Walks lane j's batch; writes its verdict and index_count into its result
