@@ -1323,7 +1323,7 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
     }
     // batches of many records, a wavefront each, after the lane walks
     {
-        const uint32_t wg = (n < 2048u ? (n + 3) / 4 : 512u);
+        const uint32_t wg = (n < 512u ? (n + 3) / 4 : 128u);  // 512 waves: a list is rare and short
         walk_wave_kernel<<<wg, 256, 0, ws>>>(d_descs, d_data, d_res, d_index, local_first, caps, block_sum, index_cap,
                                              ww.list, ww.count, ww.count + 1);
         if ((e = hipGetLastError()) != hipSuccess) return e;
