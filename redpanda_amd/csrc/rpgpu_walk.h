@@ -234,11 +234,17 @@ __device__ __forceinline__ void walk_batch(const uint8_t* __restrict__ data, Wal
 
 // ---- wave walk: batches of many records (walk_wave_kernel) -----------------
 // A lane walks its batch one record at a time, each record a dependent window
-// read: a 1 MiB batch of 17-byte records is ~60,000 of them in a row.  Above
-// kWaveWalkMin records a wavefront walks the batch instead:
+// read: a 1 MiB batch of 17-byte records is ~60,000 of them in a row, one of
+// 1,024 x 1 KiB records ~4 ms (C5).  Above kWaveWalkMin records a wavefront
+// walks the batch instead:
 //   - the record starts, from the `length` varints (record_utils.cc:183-225
-//     writes the record's size first): a wave-uniform chain over a 1 KiB
-//     chunk of the body held in the wave's registers, 64 starts at a time;
+//     writes the record's size first), up to 64 at a time, either
+//       - small records: a wave-uniform chain over a 1 KiB chunk of the body
+//         held in the wave's registers, or
+//       - records of 16 bytes or more: lane l guesses start s + l * d (d = the
+//         last record's size; a producer's records are mostly one size), reads
+//         the length there, and the guesses up to the first record whose size
+//         is not d are the chain -- one load round trip per 64 equal records;
 //   - each lane walks one record from its start exactly as walk_record does
 //     (the reference never navigates by the length, model/record.h:668-691)
 //     and the record counts only if its walk ends where the next start is;
@@ -246,7 +252,7 @@ __device__ __forceinline__ void walk_batch(const uint8_t* __restrict__ data, Wal
 // Any disagreement (a negative or overlong length, a record that fails, a
 // field walk that does not end at the next start) hands the batch to the
 // serial walk (lane 0, walk_batch), so verdicts and entries are the walk's.
-constexpr int32_t kWaveWalkMin = 1024;
+constexpr int32_t kWaveWalkMin = 64;
 
 // dword q of the 1 KiB chunk the wave holds (lane q / 4, component q % 4)
 __device__ __forceinline__ uint32_t chunk_dword(const u32x4& C, uint32_t q) {
@@ -284,17 +290,50 @@ __device__ __forceinline__ void wave_walk_batch(const uint8_t* __restrict__ data
     int64_t i = 0;        // records verified
     int64_t cb = -4096;   // body offset of the chunk in C
     u32x4 C = {0, 0, 0, 0};
+    int64_t d = 0;        // the last record's size (length varint + length)
+    uint32_t gs = 64;     // records the last stride guess found
     bool ok = true;
     while (ok && i < (int64_t)J.rc) {
         // ---- up to 64 starts, chained through the length varints
         uint32_t vstart = 0, vnext = 0;
         uint32_t g = 0;
+        if (d >= 16 && gs >= 8) {  // (after a short guess one chunk group first)
+            // stride guess: lane l reads the length at s + l * d
+            const int64_t p = s + (int64_t)l * d;
+            const bool inb = p < n;  // readable: the body's 64-byte tail pad
+            const u32x4 w = inb ? ld16(body + p) : (u32x4){0, 0, 0, 0};
+            const int64_t avail = n - p;
+            uint32_t nb = 0;
+            const int64_t len = varlong12(((uint64_t)w.y << 32) | w.x, w.z, inb ? (avail < 10 ? (uint32_t)avail : 10u) : 0u, nb);
+            const bool bad = !inb || len < 0 || len > avail;
+            const int64_t nxt = p + (int64_t)nb + len;
+            // the first lane whose record is not d long (or the last record, or lane 63)
+            const bool stop = bad || nxt != p + d || i + (int64_t)l + 1 >= (int64_t)J.rc || l == 63;
+            const uint32_t m = (uint32_t)__builtin_ctzll(__ballot(stop));
+            if (__builtin_amdgcn_readlane((int)bad, (int)m)) {  // the chain fails: the serial walk decides
+                ok = false;
+                break;
+            }
+            const int64_t sm = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)nxt >> 32), (int)m) << 32) |
+                                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)nxt, (int)m));
+            g = m + 1;
+            gs = g;
+            vstart = (uint32_t)p;
+            vnext = (uint32_t)nxt;
+            d = sm - (s + (int64_t)m * d);
+            s = sm;
+        } else {
+            gs = 64;
+        }
+        // the chunk chain (filling up a short guess's group from the chunk held)
         while (g < 64 && i + g < (int64_t)J.rc) {
             if (s >= n) {  // the chain ran off the body: the serial walk decides
                 ok = false;
                 break;
             }
-            if (s < cb || s + 12 > cb + 1024) {
+            const bool reload = s < cb || s + 12 > cb + 1024;
+            if (reload && g > 0 && d >= 16) break;  // records this size: the next group guesses
+            if (reload) {
                 cb = s & ~(int64_t)15;
                 // lanes past the body's readable end (its 64-byte tail) load nothing
                 C = cb + 16 * (int64_t)l + 16 <= n + 64 ? ld16(body + cb + 16 * l) : (u32x4){0, 0, 0, 0};
@@ -315,6 +354,7 @@ __device__ __forceinline__ void wave_walk_batch(const uint8_t* __restrict__ data
             const int64_t next = s + nb + len;
             vstart = l == g ? (uint32_t)s : vstart;
             vnext = l == g ? (uint32_t)next : vnext;
+            d = next - s;
             s = next;
             g++;
         }

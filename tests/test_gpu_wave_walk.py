@@ -1,8 +1,10 @@
 """the wave walk of batches with many records
 (rpgpu_walk.h wave_walk_batch, walk_wave_kernel).  Batches above
-kWaveWalkMin (1,024) records are walked by a wavefront: record starts chained
-through the length varints, 64 records walked at once by the lanes, each
-checked against the next start, any disagreement handed to the serial walk.
+kWaveWalkMin (64) records are walked by a wavefront: record starts chained
+through the length varints (a chain over a 1 KiB chunk for small records, a
+stride guess for records of 16 bytes or more), 64 records walked at once by
+the lanes, each checked against the next start, any disagreement handed to
+the serial walk.
 Compared field by field with the oracle (model/record.h:668-691 over
 model/record_utils.cc:116-176, oracle/batch.c): ~1 MiB batches of 7-20 byte
 records, wire and on-disk, with headers and null keys, and malformed
@@ -62,6 +64,41 @@ def malformed(rng, recs, kind):
         _, nb = orc.read_varlong(r, 0)
         recs[k] = zz(1 << 40) + r[nb:]
     return recs, rc
+
+
+def sized_records(rng, n, mode):
+    """Records of 16 bytes or more (the stride guesses): mode 0 one size
+    (1 KiB values, as C5 builds them), 1 random sizes, 2 one size with every
+    50th record longer, 3 small and large alternating."""
+    out = []
+    for j in range(n):
+        if mode == 0:
+            vl = 999
+        elif mode == 1:
+            vl = int(rng.integers(10, 300))
+        elif mode == 2:
+            vl = 120 if j % 50 else 400
+        else:
+            vl = 3 if j % 2 else 500
+        out.append(record(b"k" * 8, bytes(rng.integers(65, 91, vl, dtype=np.uint8)), ts_delta=j, off_delta=j))
+    return out
+
+
+@pytest.mark.parametrize("fmt", [WIRE, DISK])
+def test_wave_walk_sized_records(eng, fmt):
+    rng = np.random.default_rng(91 + fmt)
+    bs = []
+    for i in range(32):
+        n = [65, 66, 130, 1024, int(rng.integers(65, 3000))][i % 5]
+        recs, rc = malformed(rng, sized_records(rng, n, i % 4), (i // 4) % 8)
+        bs.append(batch(recs, fmt=fmt, base_offset=i * 10000, record_count=rc))
+    bs.insert(3, batch(sized_records(rng, 64, 0), fmt=fmt))  # 64 records: a lane walk
+    data, descs = arena(bs, fmt=fmt)
+    got = eng.submit(data, descs)
+    want = orc.validate_arena(data, descs, nthreads=8)
+    assert_same(*got, *want)
+    v = want[0]["verdict"]
+    assert (v == 0).sum() >= 8 and len(np.unique(v)) >= 4, np.unique(v)
 
 
 @pytest.mark.parametrize("fmt", [WIRE, DISK])
