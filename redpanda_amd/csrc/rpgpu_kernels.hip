@@ -1275,9 +1275,6 @@ hipError_t launch_block_scan(uint64_t* block_sum, uint32_t nb, uint64_t* total, 
 // the next chunk is checksummed.  The walk is latency-bound, the checksum
 // bandwidth-bound; they share the CUs (ov->grid: a checksum grid that leaves
 // wave slots for the walk).
-#ifndef RPGPU_CHUNK_ROUNDS
-#define RPGPU_CHUNK_ROUNDS 1
-#endif
 hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                       rpgpu_batch_result* d_res, rpgpu_record_index* d_index, uint64_t index_cap,
                       const void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s,
@@ -1308,22 +1305,8 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
     const uint32_t chunks = (ov && n >= kRunChunkMin) ? (uint32_t)ov->chunks : 1u;
     if ((e = hipMemsetAsync(ww.count, 0, 2 * sizeof(uint32_t), s)) != hipSuccess) return e;
     hipStream_t ws = s;  // the walks' stream
-    // chunk boundaries on whole rounds of the grid's waves (one batch per wave
-    // per round), so that no chunk ends with a partial round: every chunk but
-    // the last takes the same number of batches per wave
-    uint64_t per = 0;
-#if RPGPU_CHUNK_ROUNDS
-    const uint64_t waves = (uint64_t)grid * kWavesPerBlock;
-    if (chunks > 1 && (uint64_t)n >= (uint64_t)chunks * waves)
-        per = ((n + (uint64_t)chunks * waves - 1) / ((uint64_t)chunks * waves)) * waves;
-#endif
     for (uint32_t k = 0; k < chunks; k++) {
-        uint32_t lo = (uint32_t)((uint64_t)n * k / chunks), hi = (uint32_t)((uint64_t)n * (k + 1) / chunks);
-        if (per) {
-            lo = (uint32_t)std::min<uint64_t>(n, per * k);
-            hi = k + 1 == chunks ? n : (uint32_t)std::min<uint64_t>(n, per * (k + 1));
-            if (lo == hi) continue;
-        }
+        const uint32_t lo = (uint32_t)((uint64_t)n * k / chunks), hi = (uint32_t)((uint64_t)n * (k + 1) / chunks);
         const uint32_t need = (hi - lo + kWavesPerBlock - 1) / kWavesPerBlock;
         const uint32_t g = (uint32_t)grid < need ? (uint32_t)grid : need;
         validate_kernel<<<g, kValidateThreads, 0, s>>>(d_descs, lo, hi, d_data, d_res, d_index, local_first, caps,
