@@ -255,7 +255,8 @@ def main() -> int:
                     help="record payload of the compressed configs (text: Zipf words, alnum: random)")
     ap.add_argument("--walk-chunks", type=int, default=0, help="rpgpu_opts.walk_chunks (tuning; 0 = default)")
     ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
-                    help="RPGPU_OPT_WALK_OVERLAP (auto: on for the uncompressed configs)")
+                    help="the record walk beside the checksums (auto: the library default, on; "
+                         "off: RPGPU_OPT_NO_WALK_OVERLAP)")
     ap.add_argument("--blocks-per-cu", type=int, default=0, help="rpgpu_opts.blocks_per_cu (tuning; 0 = default)")
     args = ap.parse_args()
 
@@ -283,8 +284,9 @@ def main() -> int:
         spec.payload = abi.PAYLOAD_TEXT if args.payload == "text" else abi.PAYLOAD_ALNUM
     if args.ops:
         spec.ops = args.ops
-    # chunked checksum / walk overlap for the uniform uncompressed arenas (RPGPU_OPT_WALK_OVERLAP)
-    overlap = (not decompress) if args.overlap == "auto" else args.overlap == "on"
+    # the chunked checksum / walk overlap is the library's default (C3 / C4 / C5 within 1 %
+    # of serial validate-then-walk, C2 ~9 % faster; profiles/r4/NOTES.md r4i / r4j)
+    overlap = args.overlap != "off"
     eng = engine.Engine(local, walk_overlap=overlap, decomp_ws_lanes=cfg.get("ws_lanes", 0),
                         walk_chunks=args.walk_chunks, blocks_per_cu=args.blocks_per_cu)
     chunks, P_total, part_shift, (plo, phi) = rank_chunks(cfg, rank, world, scaling, args.batches)

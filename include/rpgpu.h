@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RPGPU_ABI_VERSION 3
+#define RPGPU_ABI_VERSION 4
 #define RPGPU_ARENA_TAIL_PAD 64
 #define RPGPU_HEADER_SIZE 61 /* model/record.h:527-540 */
 
@@ -185,13 +185,16 @@ typedef struct rpgpu_rp_header {
 #pragma pack(pop)
 
 /* rpgpu_opts.flags */
-/* Checksum an arena in chunks and walk each chunk's records on a second
- * stream beside the next chunk's checksums.  Pays off for arenas of many small
- * batches of similar size (the produce path: C2 4.94 vs 5.17 ms per 1M batches);
- * arenas holding large batches, whose record walks are long serial chains, run
- * slower (C5 499 vs 434 ms), because each chunk's walks then wait for the
- * previous chunk's longest one. */
+/* The record walk overlaps the checksums (the default since ABI 4): arenas of
+ * at least 16,384 batches are checksummed in rpgpu_opts.walk_chunks chunks and
+ * each chunk's records are walked on a second stream beside the next chunk's
+ * checksums (C2 4.33 vs 4.76 ms per 1M batches).  Batches of more than 64
+ * records are walked by a wavefront each after the chunks, so a chunk's walk
+ * is never a long serial chain (C5 435 vs 431 ms without the overlap, 491
+ * before the wave walk).  RPGPU_OPT_WALK_OVERLAP states the default;
+ * RPGPU_OPT_NO_WALK_OVERLAP checksums the whole arena, then walks it. */
 #define RPGPU_OPT_WALK_OVERLAP 1u
+#define RPGPU_OPT_NO_WALK_OVERLAP 2u
 
 typedef struct rpgpu_opts {
     uint32_t flags;        /* RPGPU_OPT_* */
@@ -211,7 +214,7 @@ typedef struct rpgpu_opts {
      * gzip batches (an LZ4 or snappy topic) sets a small value (minimum 256):
      * its zstd / gzip batches still decode, each lane taking more of them. */
     uint32_t decomp_ws_lanes;
-    /* RPGPU_OPT_WALK_OVERLAP: k > 1 = the arena checksummed in k chunks, each
+    /* the walk overlap: k > 1 = the arena checksummed in k chunks, each
      * chunk's walk beside the next chunk's checksums (0 = 16; at most 256);
      * 1 = checksums and speculative record walks side by side over the whole
      * arena, one launch each (slower on C2: 4.97 vs 4.26 ms per step). */

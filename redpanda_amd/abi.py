@@ -22,7 +22,8 @@ OP_HDRCRC = 2
 OP_PARSE = 4
 OP_INDEX = 8
 OP_DECOMP = 16
-OPT_WALK_OVERLAP = 1  # rpgpu_opts.flags: RPGPU_OPT_WALK_OVERLAP
+OPT_WALK_OVERLAP = 1  # rpgpu_opts.flags: RPGPU_OPT_WALK_OVERLAP (the default)
+OPT_NO_WALK_OVERLAP = 2  # RPGPU_OPT_NO_WALK_OVERLAP
 OP_RECRC = 32
 OPS_PRODUCE = OP_CRC | OP_HDRCRC | OP_PARSE | OP_INDEX
 
@@ -58,7 +59,7 @@ RPGPU_OK = 0
 RPGPU_PENDING = 1
 RPGPU_EINVAL = -1
 RPGPU_ECAPACITY = -4
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 DESC_NULL_RECORDS = 1  # rpgpu_batch_desc.flags
 

@@ -222,7 +222,7 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
         delete c;
         return nullptr;
     }
-    // RPGPU_OPT_WALK_OVERLAP: chunked (the default, 16 chunks) or checksums and
+    // the walk overlap: chunked (the default, 16 chunks) or checksums and
     // walks side by side (walk_chunks 1): C2 4.26 vs 4.97 / 4.50 ms per step
     // (5 / 6 checksum workgroups per CU, profiles/r4/NOTES.md r4b)
     c->overlap.chunks = 16;
@@ -239,8 +239,8 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
     for (int k = 0; c->have_overlap && k <= c->overlap.chunks; k++)
         c->have_overlap = hipEventCreateWithFlags(&c->overlap.ev[k], hipEventDisableTiming) == hipSuccess;
     // the walk of chunk k beside the checksums of chunk k + 1:
-    // RPGPU_OPT_WALK_OVERLAP
-    const bool want_overlap = opts && (opts->flags & RPGPU_OPT_WALK_OVERLAP);
+    // on unless RPGPU_OPT_NO_WALK_OVERLAP
+    const bool want_overlap = !(opts && (opts->flags & RPGPU_OPT_NO_WALK_OVERLAP));
     if (!want_overlap) c->have_overlap = false;
     std::vector<uint32_t> t(rpgpu::kTableWords);
     rpgpu::build_tables(t.data());

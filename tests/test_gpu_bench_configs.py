@@ -52,7 +52,7 @@ def test_uncompressed_config(name, n):
 
     cfg, spec = spec_of(name)
     data, descs = engine.build_arena(spec, n)
-    with engine.Engine(0, walk_overlap=name == "c2") as e:
+    with engine.Engine(0) as e:  # the default walk overlap
         got = e.submit(data, descs)
         again = e.submit(data, descs)
     want = orc.validate_arena(data, descs, nthreads=T)

@@ -73,15 +73,16 @@ def test_crc32c_scalar_mirror(eng):
         assert eng.crc32c_extend(seed, b) == orc.crc32c(b, seed), n
 
 
-@pytest.mark.parametrize("chunks", [0, 16])
+@pytest.mark.parametrize("chunks", [-1, 0, 1, 7])
 @pytest.mark.parametrize("case", ["headers", "ragged", "corrupt", "disk_corrupt"])
 def test_walk_overlap_arenas(case, chunks):
-    """RPGPU_OPT_WALK_OVERLAP on an arena above kRunChunkMin (16384 batches):
-    checksums and speculative walks side by side with the per-batch handshake
-    (chunks 0), or chunked checksums with each chunk's walk on a second stream
-    (16).  Results and index as the oracle's (uniform small batches, ragged
-    ones whose walks differ in length, corrupted ones -- wire and on-disk --
-    whose speculative walks must not count), on two launches in a row."""
+    """The walk overlap on an arena above kRunChunkMin (16384 batches):
+    chunked checksums with each chunk's walk on a second stream (walk_chunks
+    0 = the default 16, and 7), checksums and speculative walks side by side
+    with a merge (1), and no overlap (-1: RPGPU_OPT_NO_WALK_OVERLAP).  Results
+    and index as the oracle's (uniform small batches, ragged ones whose walks
+    differ in length, corrupted ones -- wire and on-disk -- whose speculative
+    walks must not count), on two launches in a row."""
     if case in ("corrupt", "disk_corrupt"):
         kw = dict(CASES["headers"], corrupt_ppm=50_000, corrupt_mask=0x1FF)
     else:
@@ -91,7 +92,7 @@ def test_walk_overlap_arenas(case, chunks):
     fmt = abi.FMT_RP_DISK if case == "disk_corrupt" else abi.FMT_KAFKA_WIRE
     spec = engine.make_spec(seed=zlib.crc32(case.encode()) + 7, format=fmt, **kw)
     data, descs = engine.build_arena(spec, 20000)
-    with engine.Engine(0, walk_overlap=True, walk_chunks=chunks) as e:
+    with engine.Engine(0, walk_overlap=chunks >= 0, walk_chunks=max(chunks, 0)) as e:
         got = e.submit(data, descs)
         again = e.submit(data, descs)
     want = orc.validate_arena(data, descs)
