@@ -365,13 +365,14 @@ def main() -> int:
     table = [None]
 
     def step(timed: bool):
-        eng.plan_device(d_descs.data_ptr(), n, data.data_ptr(), d_used.data_ptr(), d_scratch.data_ptr(), sh)
         if timed:
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        eng.run_device(d_descs.data_ptr(), n, data.data_ptr(), d_res.data_ptr(),
-                       d_index.data_ptr(), index_cap, d_scratch.data_ptr(), sh)
+        # plan + checksums + walk in one call (rpgpu_validate_device): with the walk
+        # overlap the plan runs on the walks' stream beside the first checksums
+        eng.validate_device(d_descs.data_ptr(), n, data.data_ptr(), d_res.data_ptr(), d_index.data_ptr(),
+                            index_cap, d_used.data_ptr(), d_scratch.data_ptr(), sh)
         if decompress:
             eng.decomp_plan_device(d_descs.data_ptr(), n, data.data_ptr(), d_res.data_ptr(),
                                    d_obytes.data_ptr(), d_dscr.data_ptr(), sh)

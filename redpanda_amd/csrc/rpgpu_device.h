@@ -9,6 +9,7 @@
 #include "rpgpu_internal.h"
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 namespace rpgpu {
 

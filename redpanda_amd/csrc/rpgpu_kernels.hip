@@ -489,8 +489,9 @@ __global__ __launch_bounds__(kValidateThreads) void validate_kernel(
         // one; has_next masks its use): a conditionally initialised struct
         // is lowered to scratch memory
         const rpgpu_batch_desc nd = sload_desc(descs + (has_next ? b + nw : b));
-        const uint64_t first = sload(block_base + b / kScanBlock) + sload(local_first + b);
-        process_batch(sT, d, b, data, res, (uint32_t)first, pf, nd, has_next DIAG_PASS);
+        // index_first is the walk's to write (walk_kernel / walk_merge_kernel): the
+        // checksums do not wait for the plan
+        process_batch(sT, d, b, data, res, 0u, pf, nd, has_next DIAG_PASS);
         STAMP(5);
     }
 #ifdef RPGPU_DIAG_STAMPS
@@ -519,11 +520,13 @@ __global__ __launch_bounds__(256) void walk_kernel(const rpgpu_batch_desc* __res
     J.base_offset = J.first_ts = 0;
     J.n = J.first = J.cap = J.b = 0;
     J.rc = 0;
+    uint32_t first_all = 0;  // every batch's index_first (validate_kernel leaves it 0)
     if (b < n) {
         const rpgpu_batch_desc d = descs[b];
         const rpgpu_batch_result& r = res[b];
+        const uint64_t first = block_base[b / kScanBlock] + local_first[b];
+        first_all = (uint32_t)first;
         if ((d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX)) && r.verdict == RPGPU_V_OK && r.codec == 0) {
-            const uint64_t first = block_base[b / kScanBlock] + local_first[b];
             uint64_t cap = caps[b];
             if (first >= index_cap) cap = 0;
             else if (first + cap > index_cap) cap = index_cap - first;
@@ -543,6 +546,7 @@ __global__ __launch_bounds__(256) void walk_kernel(const rpgpu_batch_desc* __res
         }
     }
     walk_lanes(data, J, index, res);
+    if (b < n && !(J.flags & kJobLive)) reinterpret_cast<uint32_t*>(res + b)[14] = first_all;  // .index_first
 }
 
 // The batches walk_kernel listed (more than kWaveWalkMin records): one
@@ -674,9 +678,12 @@ __global__ __launch_bounds__(256) void walk_spec_kernel(const rpgpu_batch_desc* 
 // OK, uncompressed, and ask for a walk (walk_kernel's condition).
 __global__ __launch_bounds__(256) void walk_merge_kernel(const rpgpu_batch_desc* __restrict__ descs, uint32_t n,
                                                          rpgpu_batch_result* __restrict__ res,
-                                                         const uint64_t* __restrict__ side) {
+                                                         const uint64_t* __restrict__ side,
+                                                         const uint32_t* __restrict__ local_first,
+                                                         const uint64_t* __restrict__ block_base) {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= n) return;
+    reinterpret_cast<uint32_t*>(res + b)[14] = (uint32_t)(block_base[b / kScanBlock] + local_first[b]);
     const rpgpu_batch_result& r = res[b];
     if ((descs[b].ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX)) && r.verdict == RPGPU_V_OK && r.codec == 0) {
         const uint64_t w = side[b];
@@ -1299,7 +1306,7 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if ((e = hipEventRecord(ov->ev[1], ov->aux)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(s, ov->ev[1], 0)) != hipSuccess) return e;
-        walk_merge_kernel<<<(n + 255) / 256, 256, 0, s>>>(d_descs, n, d_res, side);
+        walk_merge_kernel<<<(n + 255) / 256, 256, 0, s>>>(d_descs, n, d_res, side, local_first, block_sum);
         return hipGetLastError();
     }
     const uint32_t chunks = (ov && n >= kRunChunkMin) ? (uint32_t)ov->chunks : 1u;
@@ -1323,7 +1330,9 @@ hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t
     }
     // batches of many records, a wavefront each, after the lane walks
     {
-        const uint32_t wg = (n < 512u ? (n + 3) / 4 : 128u);  // 512 waves: a list is rare and short
+        // 1,024 waves from the queue (C5 lists ~7,600 batches of 65..1,024 records:
+        // 1.75 ms at 512 waves); an empty list costs each wave one load
+        const uint32_t wg = (n < 1024u ? (n + 3) / 4 : 256u);
         walk_wave_kernel<<<wg, 256, 0, ws>>>(d_descs, d_data, d_res, d_index, local_first, caps, block_sum, index_cap,
                                              ww.list, ww.count, ww.count + 1);
         if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1339,8 +1348,17 @@ hipError_t launch_validate(const rpgpu_batch_desc* d_descs, uint32_t n, const ui
                            rpgpu_batch_result* d_res, rpgpu_record_index* d_index, uint64_t index_cap,
                            uint64_t* d_index_used, void* d_scratch, const uint32_t* d_tables, int grid,
                            hipStream_t s, const Overlap* ov) {
-    hipError_t e = launch_plan(d_descs, n, d_data, d_index_used, d_scratch, s);
-    if (e != hipSuccess) return e;
+    hipError_t e;
+    if (ov && n >= kRunChunkMin) {
+        // the plan (index slices) on the walks' stream: only the walks read it,
+        // so the first checksums start at once (launch_run's closing join makes
+        // d_index_used visible on s with the walks)
+        if ((e = hipEventRecord(ov->ev[ov->chunks], s)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(ov->aux, ov->ev[ov->chunks], 0)) != hipSuccess) return e;
+        if ((e = launch_plan(d_descs, n, d_data, d_index_used, d_scratch, ov->aux)) != hipSuccess) return e;
+    } else if ((e = launch_plan(d_descs, n, d_data, d_index_used, d_scratch, s)) != hipSuccess) {
+        return e;
+    }
     return launch_run(d_descs, n, d_data, d_res, d_index, index_cap, d_scratch, d_tables, grid, s, ov);
 }
 

@@ -410,8 +410,8 @@ __device__ __forceinline__ void walk_lanes(const uint8_t* __restrict__ data, Wal
     walk_batch(data, J, index, verdict, cnt);
     if (J.flags & kJobLive) {
         uint32_t* r = reinterpret_cast<uint32_t*>(res + J.b);
-        r[0] = (uint32_t)verdict;  // .verdict
-        r[15] = cnt;               // .index_count
+        r[0] = (uint32_t)verdict;                                            // .verdict
+        *reinterpret_cast<u32x2*>(r + 14) = (u32x2){J.first, cnt};          // .index_first, .index_count
     }
 }
 

@@ -1,7 +1,8 @@
 """Per-launch HBM traffic of a decompress pipeline from rocprofv3 PMC passes
 (scripts/gpu_pmc_traffic.sh with --steps 1 --warmup 0): FETCH_SIZE and
 WRITE_SIZE (KB, summed over the device) of every rpgpu:: kernel dispatch of
-the one timed step, merged into profiles/traffic.json under the config.
+the one timed step (all walk-overlap chunks included), merged into
+profiles/traffic.json under the config.
 
 FETCH_SIZE is reported raw: the decoders' reads are scattered 16-byte
 accesses, for which MI355X_MICROARCH.md's 2x streaming-read correction is
@@ -19,30 +20,24 @@ from collections import defaultdict
 root, cfg, nb = sys.argv[1], sys.argv[2], int(sys.argv[3])
 payload = sys.argv[4] if len(sys.argv) > 4 else "text"
 key = cfg if payload == "text" else f"{cfg}:{payload}"
-# mean per dispatch of each kernel, times its launches per pipeline step (the
-# validation and the walk run twice: over the compressed and the rewritten
-# batches; the run may hold extra dispatches outside the step)
-tot = defaultdict(lambda: defaultdict(float))
-disp = defaultdict(lambda: defaultdict(set))
+# one pipeline step: uncompressed configs run only the step (--steps 1 --warmup 0),
+# every dispatch counts; a decompress config's bench first runs the validation
+# and the decompress plan untimed (to size the output), so its step starts at
+# the second-to-last caps_kernel (the step's plan; the last one plans the
+# rewritten batches) and every rpgpu:: dispatch from there on counts
+plain = cfg in ("c1", "c2")
+per = defaultdict(lambda: defaultdict(float))
 for f in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True)):
-    for row in csv.DictReader(open(f)):
-        k = row.get("Kernel_Name", "")
-        if "rpgpu::" not in k:
-            continue
-        name = k.split("(")[0]
-        tot[row["Counter_Name"]][name] += float(row["Counter_Value"])
-        disp[row["Counter_Name"]][name].add(row["Dispatch_Id"])
-per = defaultdict(dict)
-plain = cfg in ("c1", "c2")  # uncompressed: one step's validate / walk chunks, nothing else counted
-for c in tot:
-    for name, v in tot[c].items():
-        hot = "validate_kernel" in name or "walk_kernel" in name
-        if plain:
-            if hot:
-                per[c][name] = v  # every chunk dispatch of the one step (--steps 1 --warmup 0)
-            continue
-        calls = 2 if hot else 1
-        per[c][name] = v / len(disp[c][name]) * calls
+    rows = [r for r in csv.DictReader(open(f)) if "rpgpu::" in r.get("Kernel_Name", "")]
+    start = 0
+    if not plain:
+        caps = sorted({int(r["Dispatch_Id"]) for r in rows if r["Kernel_Name"].startswith("rpgpu::caps_kernel")})
+        start = caps[-2] if len(caps) >= 2 else 0
+    for r in rows:
+        if plain and not any(k in r["Kernel_Name"] for k in ("validate_kernel", "walk_kernel", "walk_wave_kernel")):
+            continue  # the roofline's kernels: the checksums and the walk
+        if int(r["Dispatch_Id"]) >= start:
+            per[r["Counter_Name"]][r["Kernel_Name"].split("(")[0]] += float(r["Counter_Value"])
 fetch = sum(v * (2.0 if "validate_kernel" in k else 1.0) for k, v in per["FETCH_SIZE"].items()) * 1024
 write = sum(per["WRITE_SIZE"].values()) * 1024
 out = {"batches": nb, "payload": payload,
