@@ -68,7 +68,6 @@ CONFIGS = {
                  "LZ4F decompression, batch rewrite with fresh CRCs, record walk + index of the "
                  "decompressed records",
         batches=1 << 18, partitions=4096, decompress=True, cpu_sample=2048,
-        ws_lanes=256,  # an LZ4 reader: the minimum of zstd / gzip workspaces (rpgpu_opts.decomp_ws_lanes)
         spec=dict(records_per_batch=64, key_len=16, value_len=999, codec=3)),
     "c4": dict(
         workload="C4: zstd-compressed Kafka v2 batches (the reference's compressor: level 3, pledged "

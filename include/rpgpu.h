@@ -208,11 +208,11 @@ typedef struct rpgpu_opts {
      * limit: there the outcome depends on the broker's free memory. */
     uint64_t max_decoded_batch;
     /* decompression: ceiling on the zstd / gzip decoder lanes, each with a
-     * ~20 KB workspace in the scratch (rpgpu_decomp_scratch_bytes_ctx).
-     * 0 = 131072 zstd / 32768 gzip lanes (2.6 GB for arenas of >= 131072
-     * batches: the C4 tuning); a reader whose arenas carry few or no zstd /
-     * gzip batches (an LZ4 or snappy topic) sets a small value (minimum 256):
-     * its zstd / gzip batches still decode, each lane taking more of them. */
+     * workspace (zstd ~19 KB, after the output slots, one per zstd batch up
+     * to the ceiling; gzip 2 KB, in the scratch: rpgpu_decomp_scratch_bytes_ctx).
+     * 0 = 131072 zstd / 32768 gzip lanes (the C4 tuning); a smaller value
+     * (minimum 256) bounds the memory: the batches still decode, each lane
+     * taking more of them. */
     uint32_t decomp_ws_lanes;
     /* the walk overlap: k > 1 = the arena checksummed in k chunks, each
      * chunk's walk beside the next chunk's checksums (0 = 16; at most 256);
@@ -372,19 +372,26 @@ typedef struct rpgpu_decomp_result {
                             the decoded size + slack)                         */
 } rpgpu_decomp_result;   /* 32 bytes */
 
-/* Scratch of the decompress path: the plan's slots and scans, the validation
- * scratch of the rewritten batches, one ~20 KB zstd workspace per decoder
- * lane (min(n, 131072) lanes: up to 2.6 GB, sized for HBM, not for the host;
- * fewer with rpgpu_opts.decomp_ws_lanes, see rpgpu_decomp_scratch_bytes_ctx)
- * and the part list of split bodies (36 B per part, n + 4096 parts). */
+/* Scratch of the decompress path: the plan's slots, lists and scans, the
+ * validation scratch of the rewritten batches, the wave decoders' literal
+ * buffers, one 2 KB gzip workspace per gzip lane (min(n, 32768), fewer with
+ * rpgpu_opts.decomp_ws_lanes, see rpgpu_decomp_scratch_bytes_ctx) and the part
+ * list of split bodies (36 B per part, n + 4096 parts).  The zstd lane
+ * workspaces (~19 KB each) are not in it: the plan counts the arena's zstd
+ * batches and puts one workspace per batch (at most 131,072, or
+ * decomp_ws_lanes) after the output slots, so an arena without zstd batches
+ * reserves none (ABI 4). */
 size_t rpgpu_decomp_scratch_bytes(uint32_t n);
 /* The same for a context's rpgpu_opts.decomp_ws_lanes (never more than
  * rpgpu_decomp_scratch_bytes(n)); the scratch of a context's decompress calls
  * must hold at least this. */
 size_t rpgpu_decomp_scratch_bytes_ctx(const rpgpu_ctx* ctx, uint32_t n);
 /* Plan: per-batch output slots and their exclusive scan into d_scratch;
- * *d_out_bytes = output bytes needed.  The output buffer must hold
- * *d_out_bytes + RPGPU_ARENA_TAIL_PAD bytes. */
+ * *d_out_bytes = output bytes needed: the slots, then (256-byte aligned) the
+ * zstd lane workspaces.  The output buffer must hold *d_out_bytes +
+ * RPGPU_ARENA_TAIL_PAD bytes; with less, batches whose slot does not fit get
+ * RPGPU_V_DECOMP_OVERFLOW, and so do the zstd lane batches when the
+ * workspaces do not fit. */
 int32_t rpgpu_decomp_plan_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_descs, uint32_t n,
                                  const uint8_t* d_data, const rpgpu_batch_result* d_results,
                                  uint64_t* d_out_bytes, void* d_scratch, void* hip_stream);

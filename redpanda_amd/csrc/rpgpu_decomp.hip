@@ -59,15 +59,14 @@ constexpr uint64_t kLitScratch = (128u << 10) + 256;  // ZSTD_BLOCKSIZE_MAX + sl
 #define RPZ_LANES 131072  // 2 waves per SIMD at the lane kernel's VGPR count
 #endif
 constexpr uint32_t kZstdLanes = RPZ_LANES;
-union LaneWsZ {  // a zstd (or gzip) lane's workspace in HBM
-    rpzstd::Ws z;
-    rpinfl::Ws g;
-};
-// zstd and gzip lanes keep their workspaces in HBM (one region, the union):
-// zstd tables in LDS, one workspace per lane, held 20 lanes per CU against
-// 512 in HBM and measured 3.25 s vs 0.585 s per C4 step (round 3: the lane's
-// chain of dependent global accesses per sequence, not its table lookups,
-// sets its pace); gzip is in no benchmark configuration
+// zstd and gzip lanes keep their workspaces in HBM: zstd tables in LDS, one
+// workspace per lane, held 20 lanes per CU against 512 in HBM and measured
+// 3.25 s vs 0.585 s per C4 step (round 3: the lane's chain of dependent
+// global accesses per sequence, not its table lookups, sets its pace); gzip
+// is in no benchmark configuration.  The gzip workspaces (2 KB, also used by
+// the plan's counting decode) live in the scratch; the zstd ones (~19 KB)
+// after the output slots, as many as the plan found zstd lane batches (up to
+// the cap): an arena without zstd batches reserves none
 constexpr uint32_t kGzipLanes = 32768;
 // cap: the context's ceiling on workspace lanes (rpgpu_opts.decomp_ws_lanes;
 // 0 = the defaults above, never below kMinWsLanes): an arena whose zstd / gzip
@@ -90,10 +89,7 @@ uint32_t gzip_lanes(uint32_t n, uint32_t cap) {
     const uint32_t c = lane_cap(cap, kGzipLanes);
     return n < c ? n : c;
 }
-size_t ws_region(uint32_t n, uint32_t cap) {
-    const size_t z = (size_t)zstd_lanes(n, cap) * sizeof(LaneWsZ), g = (size_t)gzip_lanes(n, cap) * sizeof(rpinfl::Ws);
-    return z > g ? z : g;
-}
+size_t ws_region(uint32_t n, uint32_t cap) { return (size_t)gzip_lanes(n, cap) * sizeof(rpinfl::Ws); }
 uint32_t decomp_waves(uint32_t n) { return n < kDecompWaves ? n : kDecompWaves; }
 // scratch: slot[n] u64 | local[n] u64 | block_sum[nb] u64 | validate scratch |
 //          counters (256 B) | wave literal scratch[waves] | lane Ws[lanes]
@@ -108,19 +104,18 @@ constexpr uint32_t kSkipPart = 0xffffffffu;  // a reserved slot without a part
 uint32_t part_cap(uint32_t n) { return 2 * ((n + 4096u) / 2); }
 struct Parts {
     uint64_t *slot, *local, *block_sum;
-    uint32_t* wlist;   // wave-owned batches: zstd [0, n), LZ [n, 2n)
+    uint32_t* wlist;   // wave-owned batches: zstd [0, n), LZ [n, 2n); zstd lane batches [2n, 3n)
     uint32_t *sfirst, *scount;  // a split batch's parts (scount 0: not split)
     SplitPart* parts;
     int32_t* pres;     // decoded size per part (-1 error, -2 no slot)
     void* vscratch;
     uint32_t* counter;
     uint8_t* lits;
-    LaneWsZ* zws;     // zstd lanes ...
-    rpinfl::Ws* gws;  // ... and gzip lanes: the same region
+    rpinfl::Ws* gws;  // gzip lanes' workspaces
 };
 size_t parts_head(uint32_t n) {
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
-    return ((size_t)n * 32 + nb * 8 + 255) & ~(size_t)255;  // slot, local: 8 B; wlist: 2 x 4 B; sfirst, scount
+    return ((size_t)n * 36 + nb * 8 + 255) & ~(size_t)255;  // slot, local: 8 B; wlist: 3 x 4 B; sfirst, scount
 }
 size_t counter_offset(uint32_t n) { return (parts_head(n) + validate_scratch_bytes(n) + 255) & ~(size_t)255; }
 size_t zws_offset(uint32_t n) { return counter_offset(n) + 256 + (size_t)decomp_waves(n) * kLitScratch; }
@@ -134,12 +129,11 @@ Parts parts(void* p, uint32_t n, uint32_t cap) {
     s.local = s.slot + n;
     s.block_sum = s.local + n;
     s.wlist = reinterpret_cast<uint32_t*>(s.block_sum + (n + kScanBlock - 1) / kScanBlock);
-    s.sfirst = s.wlist + 2 * (size_t)n;
+    s.sfirst = s.wlist + 3 * (size_t)n;
     s.scount = s.sfirst + n;
     s.vscratch = b + parts_head(n);
     s.counter = reinterpret_cast<uint32_t*>(b + counter_offset(n));
     s.lits = b + counter_offset(n) + 256;
-    s.zws = reinterpret_cast<LaneWsZ*>(b + zws_offset(n));
     s.gws = reinterpret_cast<rpinfl::Ws*>(b + zws_offset(n));
     s.parts = reinterpret_cast<SplitPart*>(b + parts_offset(n, cap));
     s.pres = reinterpret_cast<int32_t*>(s.parts + part_cap(n));
@@ -314,6 +308,16 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
         sfirst[i] = sf;
         scount[i] = sc;
     }
+    // zstd batches for the lane decoder (not wave-owned; overflowing ones too,
+    // for their verdict): listed with one atomic per wave
+    const bool zl = i < n && wanted && codec == 4 && (over || sz <= lane_max(4));
+    const uint64_t zm = __ballot(zl);
+    if (zm) {
+        uint32_t zb = 0;
+        if (l == (uint32_t)__builtin_ctzll(zm)) zb = atomicAdd(wcount + 5, (uint32_t)__builtin_popcountll(zm));
+        zb = (uint32_t)__shfl(zb, __builtin_ctzll(zm), 64);
+        if (zl) wlist[2 * (size_t)n + zb + (uint32_t)__builtin_popcountll(zm & ((1ull << l) - 1))] = i;
+    }
     if (threadIdx.x == kScanBlock - 1) {
         uint64_t tot = 0;
         for (uint32_t k = 0; k < kScanBlock / 64; k++) tot += wsum[k];
@@ -465,14 +469,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_WS_WA
     const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
     rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
-    rpgpu_batch_desc* __restrict__ out_descs, void* __restrict__ wsraw) {
+    rpgpu_batch_desc* __restrict__ out_descs, void* __restrict__ wsraw, const uint32_t* __restrict__ counter,
+    const uint32_t* __restrict__ zlist) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t lanes = gridDim.x * blockDim.x;
-    if (g >= n) return;  // lanes past the arena own no workspace
-    // gzip: 2 KB workspaces; zstd (RPGPU_ZSTD_HBM): the union
-    LaneWsZ& zws = reinterpret_cast<LaneWsZ*>(wsraw)[g];
+    // gzip: every batch index, 2 KB workspaces in the scratch; zstd: the plan's
+    // list, `zl` workspaces after the output slots (decomp_ws_kernel)
+    uint32_t lanes = gridDim.x * blockDim.x, cnt = n;
+    uint64_t ws_end = 0;
+    uint8_t* zbase = nullptr;
+    if (FAM == 4) {
+        cnt = counter[7];
+        lanes = counter[10];
+        const uint64_t ws_off = (uint64_t)counter[8] | ((uint64_t)counter[9] << 32);
+        ws_end = ws_off + (uint64_t)lanes * sizeof(rpzstd::Ws);
+        zbase = out + ws_off;
+    }
+    if (g >= n || g >= lanes) return;  // lanes past the arena / the list own no workspace
     rpinfl::Ws& gws = reinterpret_cast<rpinfl::Ws*>(wsraw)[g];
-    for (uint32_t i = g; i < n; i += lanes) {
+    for (uint32_t k = g; k < cnt; k += lanes) {
+        const uint32_t i = FAM == 4 ? zlist[k] : k;
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
         uint64_t sz = slot[i];
@@ -485,14 +500,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_WS_WA
             uint8_t* o = out + off + kHeaderSize;
             const uint64_t cap = sz - kHeaderSize - rpcodec::kSlack;
             if (FAM == 4) {
-                rpzstd::DirectEmit em;
-                verdict = rpzstd::uncompress(em, in, body_len(v), o, cap, &len, zws.z);
+                if (ws_end > out_cap) {
+                    verdict = RPGPU_V_DECOMP_OVERFLOW;  // caller's buffer smaller than the plan
+                } else {
+                    rpzstd::DirectEmit em;
+                    verdict = rpzstd::uncompress(em, in, body_len(v), o, cap, &len,
+                                                 reinterpret_cast<rpzstd::Ws*>(zbase)[g]);
+                }
             } else {
                 verdict = rpinfl::uncompress(in, body_len(v), o, cap, &len, gws);
             }
         }
         finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
     }
+}
+
+// After the plan's scan: the zstd lane workspaces go after the output slots
+// (256-byte aligned), min(listed zstd lane batches, cap) of them; the plan's
+// output bytes include them.  counter[8..9] = their offset, [10] = lanes.
+__global__ void decomp_ws_kernel(uint32_t* __restrict__ counter, uint32_t cap, uint64_t* __restrict__ out_bytes) {
+    if (threadIdx.x != 0) return;
+    const uint64_t slots = (uint64_t)counter[8] | ((uint64_t)counter[9] << 32);  // the scan's total
+    const uint64_t off = (slots + 255) & ~(uint64_t)255;
+    const uint32_t lanes = counter[7] < cap ? counter[7] : cap;
+    counter[8] = (uint32_t)off;
+    counter[9] = (uint32_t)(off >> 32);
+    counter[10] = lanes;
+    if (out_bytes) *out_bytes = lanes ? off + (uint64_t)lanes * sizeof(rpzstd::Ws) : slots;
 }
 
 // One batch body through the codec restatement, bytes produced by the wave.
@@ -682,8 +716,9 @@ hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // wave-owned batch lists (filled by decomp_caps_kernel): counters 2 and 3
-    // counters 2, 3: wave list lengths; 4, 5: LZ4 / snappy parts
+    // counters 2, 3: wave list lengths; 4, 5: LZ4 / snappy parts; 7: zstd lane list
     if ((e = hipMemsetAsync(p.counter + 2, 0, 4 * sizeof(uint32_t), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(p.counter + 7, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
     decomp_caps_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
                                                  max_decoded, p.counter + 2, p.wlist, p.sfirst, p.scount, p.parts,
                                                  part_cap(n));
@@ -691,7 +726,9 @@ hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const
     if (e != hipSuccess) return e;
     decomp_counters_kernel<<<1, 64, 0, s>>>(p.counter, 0);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    return launch_block_scan(p.block_sum, nb, d_out_bytes, s);
+    if ((e = launch_block_scan(p.block_sum, nb, reinterpret_cast<uint64_t*>(p.counter + 8), s)) != hipSuccess) return e;
+    decomp_ws_kernel<<<1, 64, 0, s>>>(p.counter, zstd_lanes(n, ws_cap), d_out_bytes);
+    return hipGetLastError();
 }
 
 hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
@@ -746,13 +783,15 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     decomp_lane_kernel<2><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
                                               out_cap, d_out_descs, p.scount);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const uint32_t zl = zstd_lanes(n, ws_cap);  // the HBM-workspace lane decoder
+    const uint32_t zl = zstd_lanes(n, ws_cap);  // the HBM-workspace lane decoder (at most zl lanes)
     ws_lane_kernel<4><<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres,
-                                                         d_out, out_cap, d_out_descs, p.zws);
+                                                         d_out, out_cap, d_out_descs, nullptr, p.counter,
+                                                         p.wlist + 2 * (size_t)n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t gl = gzip_lanes(n, ws_cap);
     ws_lane_kernel<1><<<(gl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
-                                                         d_dres, d_out, out_cap, d_out_descs, p.gws);
+                                                         d_dres, d_out, out_cap, d_out_descs, p.gws, p.counter,
+                                                         nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ds) {
         if ((e = hipEventRecord(ds->join, ds->aux)) != hipSuccess) return e;

@@ -218,11 +218,18 @@ def test_many_tiny_zstd_gzip(eng):
     assert ((v == abi.V_OK) & (codec == 1)).sum() > 131_072 // 2
 
 
+def zstd_workspace_bytes(got):
+    """Output bytes past the slots (rounded to 256): the zstd lane workspaces."""
+    d = got["dres"]
+    end = int((d["out_offset"].astype(np.int64) + d["out_cap"].astype(np.int64))[d["out_cap"] > 0].max(initial=0))
+    return got["out_bytes"] - ((end + 255) & ~255) if got["out_bytes"] > end else 0
+
+
 def test_few_workspace_lanes():
-    """rpgpu_opts.decomp_ws_lanes = 256 (an LZ4 reader's small scratch): a
-    mixed arena with 6,000 zstd / gzip batches still decodes exactly as the
-    oracle, each of the 256 workspace lanes taking ~20 frames in turn, and the
-    context's scratch is a fraction of the default one."""
+    """rpgpu_opts.decomp_ws_lanes = 256: a mixed arena with 6,000 zstd / gzip
+    batches still decodes exactly as the oracle, each of the 256 workspace
+    lanes taking ~20 frames in turn; the plan's output bytes hold 256 zstd
+    workspaces, the scratch only gzip's."""
     from redpanda_amd import abi, engine
 
     spec = engine.make_spec(seed=0x5EED0078, partitions=32, codec_mix=(1 << 4) | (1 << 1) | (1 << 3),
@@ -231,11 +238,42 @@ def test_few_workspace_lanes():
     data, descs = engine.build_arena(spec, 9000)
     with engine.Engine(0, decomp_ws_lanes=256) as e:
         n = 200_000
-        assert e.decomp_scratch_bytes(n) < abi.lib().rpgpu_decomp_scratch_bytes(n) // 4
+        assert e.decomp_scratch_bytes(n) < abi.lib().rpgpu_decomp_scratch_bytes(n)
         got = e.decompress_arena(data, descs)
     compare(got, data, descs)
     v, codec = got["dres"]["verdict"], got["dres"]["codec"]
     assert ((v == abi.V_OK) & ((codec == 4) | (codec == 1))).sum() > 5000
+    ws = zstd_workspace_bytes(got)
+    assert ws % 256 == 0 and 8 << 10 < ws // 256 < 32 << 10, ws
+
+
+def test_zstd_workspaces_follow_the_plan(eng):
+    """the zstd lane workspaces sit after the output slots,
+    one per zstd lane batch the plan found (up to the cap): an LZ4 / snappy
+    arena's output is its slots alone and the scratch holds no zstd workspace;
+    k zstd batches add k workspaces; every batch decodes as the oracle."""
+    from redpanda_amd import abi
+
+    assert abi.lib().rpgpu_decomp_scratch_bytes(131072) < 1 << 30  # was ~2.6 GB with them
+    rng = np.random.default_rng(29)
+    per = []
+    for codecs, k in (((3, 2), 0), ((3, 4), 9), ((4,), 23)):
+        bodies = []
+        for j in range(40 if k == 0 else k + 15):
+            c = codecs[j % len(codecs)] if k == 0 else (4 if j < k else 3)
+            bodies.append((orc.compress(c, b"".join(records(rng, 12, 4, 200, text=True))), c))
+        bs = [batch(b, fmt=WIRE, record_count=12, attrs=c) for b, c in bodies]
+        data, descs = arena(bs, fmt=WIRE, ops=OPS)
+        got = eng.decompress_arena(data, descs)
+        compare(got, data, descs)
+        assert (got["dres"]["verdict"] == abi.V_OK).all()
+        ws = zstd_workspace_bytes(got)
+        if k == 0:
+            assert ws == 0, ws
+        else:
+            assert ws % k == 0, (ws, k)
+            per.append(ws // k)
+    assert per[0] == per[1] and 8 << 10 < per[0] < 32 << 10, per
 
 
 def test_ws_lanes_not_a_multiple_of_256():
