@@ -104,7 +104,8 @@ constexpr uint32_t kSkipPart = 0xffffffffu;  // a reserved slot without a part
 uint32_t part_cap(uint32_t n) { return 2 * ((n + 4096u) / 2); }
 struct Parts {
     uint64_t *slot, *local, *block_sum;
-    uint32_t* wlist;   // wave-owned batches: zstd [0, n), LZ [n, 2n); zstd lane batches [2n, 3n)
+    uint32_t* wlist;   // wave-owned batches: zstd [0, n), LZ [n, 2n); zstd lane batches [2n, 3n) and
+                       // the ones whose ring wrapped behind them
     uint32_t *sfirst, *scount;  // a split batch's parts (scount 0: not split)
     SplitPart* parts;
     int32_t* pres;     // decoded size per part (-1 error, -2 no slot)
@@ -115,7 +116,7 @@ struct Parts {
 };
 size_t parts_head(uint32_t n) {
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
-    return ((size_t)n * 36 + nb * 8 + 255) & ~(size_t)255;  // slot, local: 8 B; wlist: 3 x 4 B; sfirst, scount
+    return ((size_t)n * 40 + nb * 8 + 255) & ~(size_t)255;  // slot, local: 8 B; wlist: 4 x 4 B; sfirst, scount
 }
 size_t counter_offset(uint32_t n) { return (parts_head(n) + validate_scratch_bytes(n) + 255) & ~(size_t)255; }
 size_t zws_offset(uint32_t n) { return counter_offset(n) + 256 + (size_t)decomp_waves(n) * kLitScratch; }
@@ -129,7 +130,7 @@ Parts parts(void* p, uint32_t n, uint32_t cap) {
     s.local = s.slot + n;
     s.block_sum = s.local + n;
     s.wlist = reinterpret_cast<uint32_t*>(s.block_sum + (n + kScanBlock - 1) / kScanBlock);
-    s.sfirst = s.wlist + 3 * (size_t)n;
+    s.sfirst = s.wlist + 4 * (size_t)n;
     s.scount = s.sfirst + n;
     s.vscratch = b + parts_head(n);
     s.counter = reinterpret_cast<uint32_t*>(b + counter_offset(n));
@@ -469,8 +470,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_WS_WA
     const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
     rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
-    rpgpu_batch_desc* __restrict__ out_descs, void* __restrict__ wsraw, const uint32_t* __restrict__ counter,
-    const uint32_t* __restrict__ zlist) {
+    rpgpu_batch_desc* __restrict__ out_descs, void* __restrict__ wsraw, uint32_t* __restrict__ counter,
+    uint32_t* __restrict__ zlist) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     // gzip: every batch index, 2 KB workspaces in the scratch; zstd: the plan's
     // list, `zl` workspaces after the output slots (decomp_ws_kernel)
@@ -504,13 +505,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_WS_WA
                     verdict = RPGPU_V_DECOMP_OVERFLOW;  // caller's buffer smaller than the plan
                 } else {
                     rpzstd::DirectEmit em;
-                    verdict = rpzstd::uncompress(em, in, body_len(v), o, cap, &len,
-                                                 reinterpret_cast<rpzstd::Ws*>(zbase)[g]);
+                    verdict = rpzstd::uncompress<false>(em, in, body_len(v), o, cap, &len,
+                                                        reinterpret_cast<rpzstd::Ws*>(zbase)[g]);
+                    if (verdict == rpzstd::V_RING) {  // its ring wraps: zstd_ring_kernel's
+                        zlist[counter[7] + atomicAdd(counter + 11, 1u)] = i;
+                        continue;
+                    }
                 }
             } else {
                 verdict = rpinfl::uncompress(in, body_len(v), o, cap, &len, gws);
             }
         }
+        finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
+    }
+}
+
+// zstd lane batches whose ring buffer wrapped (streaming frames larger than
+// window + block + 64 bytes): decoded again with the ring's history
+// (rpzstd::uncompress<true>), after the lane kernel, on its workspaces.
+__global__ __launch_bounds__(256) void zstd_ring_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data,
+    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
+    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
+    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
+    rpgpu_batch_desc* __restrict__ out_descs, const uint32_t* __restrict__ counter,
+    const uint32_t* __restrict__ zlist) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t cnt = counter[11], lanes = counter[10] < cnt ? counter[10] : cnt;
+    if (g >= lanes) return;
+    const uint32_t* rlist = zlist + counter[7];
+    const uint64_t ws_off = (uint64_t)counter[8] | ((uint64_t)counter[9] << 32);
+    rpzstd::Ws& ws = reinterpret_cast<rpzstd::Ws*>(out + ws_off)[g];
+    for (uint32_t k = g; k < cnt; k += lanes) {
+        const uint32_t i = rlist[k];
+        const rpgpu_batch_desc d = descs[i];
+        const rpgpu_batch_result v = vres[i];
+        uint64_t sz = slot[i];
+        const uint64_t off = block_base[i / kScanBlock] + local[i];
+        uint64_t len = 0;
+        rpzstd::DirectEmit em;
+        const int32_t verdict = rpzstd::uncompress<true>(em, data + d.offset + kHeaderSize, body_len(v),
+                                                         out + off + kHeaderSize,
+                                                         sz - kHeaderSize - rpcodec::kSlack, &len, ws);
         finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
     }
 }
@@ -551,7 +587,9 @@ __device__ __forceinline__ int32_t decode_body(rpwave::WaveEmit& em, rpzstd::Ws&
 // One wavefront per batch over a persistent grid of kDecompWaves waves; each
 // wave takes the next batch from an atomic counter (skewed batch sizes: a
 // wave that drew a 1 MiB body does not hold up the batches queued behind
-// it).  The zstd workspace is the wave's LDS.
+// it).  The zstd workspace is the wave's LDS; the wave decoder carries the
+// zstd ring's history in its one pass (a first pass without it, as the lane
+// decoder does, compiled to 346 registers: C5 543 vs 427 ms).
 template <uint32_t FAM>
 __global__ __launch_bounds__(64) void decomp_wave_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
@@ -699,6 +737,7 @@ __global__ void decomp_counters_kernel(uint32_t* c, uint32_t run) {
         c[0] = 0;
         c[1] = 0;
         c[3] = c[6];
+        c[11] = 0;  // zstd lane batches whose ring wrapped
     } else {
         c[6] = c[3];
     }
@@ -787,6 +826,9 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     ws_lane_kernel<4><<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres,
                                                          d_out, out_cap, d_out_descs, nullptr, p.counter,
                                                          p.wlist + 2 * (size_t)n);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    zstd_ring_kernel<<<(zl + 255) / 256, 256, 0, s>>>(d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres,
+                                                      d_out, out_cap, d_out_descs, p.counter, p.wlist + 2 * (size_t)n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t gl = gzip_lanes(n, ws_cap);
     ws_lane_kernel<1><<<(gl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,

@@ -34,11 +34,21 @@
 //     (BIT_readBits / BIT_readBitsFast on a drained container), since a
 //     sequence stream that over-reads is still accepted by 1.4.9.
 //
-// Not restated: the ring's extDict view once the ring wraps (frames larger
-// than window + 128 KiB + 64 with no or a larger content size): history is
-// kept flat, so a CORRUPT offset that reaches past the ring's retained history
-// in such a frame is accepted here and rejected (or read from overwritten ring
-// bytes) by libzstd.  Valid frames decode identically.
+//   * the ring buffer's history once it wraps (frames larger than window +
+//     128 KiB + 64 with no or a larger content size): every segment starts at
+//     the ring's start, the previous segment is the extDict and older ones are
+//     gone (ZSTD_checkContinuity), so an offset reaching before the previous
+//     segment is corruption_detected, and one reaching into the part of the
+//     previous segment that the current one has overwritten reads the current
+//     segment's bytes there (ZSTD_execSequence's extDict copy); the output is
+//     kept flat here and such a match is rebuilt from it (block(): vstart /
+//     pstart).  Valid frames never reach either (offsets <= window).
+//
+// Not restated: libzstd's copies write up to 32-48 bytes past their end
+// (ZSTD_wildcopy / ZSTD_overlapCopy8), into the ring; an offset beyond the
+// window whose match reads the previous segment within 64 bytes past the
+// current write position reads those bytes in libzstd and the previous
+// segment's here (tests/native/zstd_fuzz.cpp in_overrun_band).
 //
 // Serial per frame: the same code runs on the host in the differential fuzz
 // (tests/native/zstd_fuzz.cpp) and on the device in one lane per batch, each
@@ -74,6 +84,10 @@ using rpcodec::le32;
 using rpcodec::le64;
 
 constexpr int32_t V_OK = 0, V_ERROR = 30, V_OVERFLOW = 34;
+// uncompress<false>: the frame's ring buffer wrapped; decode the body again
+// with uncompress<true> (the lane decoder hands such batches to
+// rpgpu_decomp.hip's zstd_ring_kernel)
+constexpr int32_t V_RING = 99;
 constexpr uint32_t kMagic = 0xFD2FB528u, kSkipMagic = 0x184D2A50u, kSkipMask = 0xFFFFFFF0u;
 constexpr uint64_t kBlockMax = 128u * 1024u;          // ZSTD_BLOCKSIZE_MAX
 constexpr uint64_t kStage = 64u * 1024u;              // stream_zstd d_buffer
@@ -273,6 +287,7 @@ struct Ws {
     uint8_t w[256];                  // Huffman weights
     uint32_t rank[kHufMaxLog + 1];
     uint64_t rep[3];
+    uint64_t ring_v, ring_p;  // the ring's previous and current segment (flat offsets)
     uint8_t ll_log, ml_log, of_log, huf_log;
     uint8_t huf_x2, lit_entropy, fse_entropy, huf1_on;
 #if RPZ_PROF
@@ -942,12 +957,32 @@ RPC_HD int64_t seq_table_impl(W& w, uint32_t mode, uint32_t which, const uint8_t
     }
 }
 
+// A match that starts in the extDict where the current ring segment has
+// overwritten it (ring offset a < lw; only offsets beyond the window get
+// here): those bytes are the current segment's, the rest reads on as in the
+// flat output.  Only blocks decoded after the ring has wrapped (block<true>)
+// check for it.
+template <class E>
+RPC_HD void ring_match(E& em, uint8_t* out, uint64_t lit_end, uint64_t offset, uint64_t ml, uint64_t vstart,
+                       uint64_t pstart) {
+    const uint64_t a = lit_end - offset - vstart, lw = lit_end - pstart, len1 = pstart - (lit_end - offset);
+    uint64_t k1 = lw - a;
+    if (k1 > len1) k1 = len1;
+    if (k1 > ml) k1 = ml;
+    em.sync();
+    em.lits(out + lit_end, out + pstart + a, k1);
+    if (ml > k1) em.match(out + lit_end + k1, offset, ml - k1);
+    else em.sync();
+}
 // ZSTD_decompressBlock_internal for one compressed block: output at out[op..),
-// history from out[fstart..), at most `cap` bytes; literals may use the slot
-// tail [.., tail).  Returns bytes produced, -1 error, -2 slot exceeded.
-template <class E, class W>
-RPZ_COLD int64_t block(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t fstart, uint64_t op,
-                       uint64_t cap, uint64_t tail) {
+// at most `cap` bytes; literals may use the slot tail [.., tail).  History:
+// the ring segment being written starts at pstart, the previous one (the
+// extDict, none if vstart == pstart) at vstart; a flat, single-pass frame has
+// vstart = pstart = its start.  kRing: the ring has wrapped (vstart < pstart).
+// Returns bytes produced, -1 error, -2 slot exceeded.
+template <bool kRing, class E, class W>
+RPZ_COLD int64_t block(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t vstart, uint64_t pstart,
+                       uint64_t op, uint64_t cap, uint64_t tail) {
     if (n >= kBlockMax) return RPZ_FAIL(-1);
     constexpr bool kLdsWs = E::kInlineBlocks;  // the wave decoders keep Ws in LDS
     Lit lit;
@@ -1050,10 +1085,17 @@ RPZ_COLD int64_t block(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out,
             if (ll + ml > oend - o) return RPZ_FAIL(-1);
             if (ll > (uint64_t)(lend - lp)) return RPZ_FAIL(-1);
             const uint64_t lit_end = o + ll;
-            if (offset > lit_end - fstart) return RPZ_FAIL(-1);
+            if (offset > lit_end - vstart) return RPZ_FAIL(-1);
             em.lits(out + o, lp, ll);
             lp += ll;
-            em.match(out + lit_end, offset, ml);
+            if constexpr (kRing) {
+                if (offset > lit_end - pstart && offset > pstart - vstart)
+                    ring_match(em, out, lit_end, offset, ml, vstart, pstart);
+                else
+                    em.match(out + lit_end, offset, ml);
+            } else {
+                em.match(out + lit_end, offset, ml);
+            }
             o = lit_end + ml;
         }
 #if RPZ_PROF
@@ -1075,19 +1117,23 @@ RPZ_COLD int64_t block(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out,
 // block() out of line for the lane decoders (DirectEmit: inlined at both call
 // sites the lane kernel outgrew the instruction cache), inline for the wave
 // emitter (its state stays in registers, its workspace accesses LDS ops).
-template <class E, class W>
+template <bool kRing, class E, class W>
 __attribute__((noinline)) RPZ_HD_NOINL int64_t block_noinline(E& em, W& w, const uint8_t* in, uint64_t n,
-                                                              uint8_t* out, uint64_t fstart, uint64_t op,
-                                                              uint64_t cap, uint64_t tail) {
-    return block(em, w, in, n, out, fstart, op, cap, tail);
+                                                              uint8_t* out, uint64_t vstart, uint64_t pstart,
+                                                              uint64_t op, uint64_t cap, uint64_t tail) {
+    return block<kRing>(em, w, in, n, out, vstart, pstart, op, cap, tail);
 }
-template <class E, class W>
-RPC_HD int64_t block_call(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t fstart, uint64_t op,
-                          uint64_t cap, uint64_t tail) {
-    if constexpr (E::kInlineBlocks)
-        return block(em, w, in, n, out, fstart, op, cap, tail);
-    else
-        return block_noinline(em, w, in, n, out, fstart, op, cap, tail);
+template <bool kRing, class E, class W>
+RPC_HD int64_t block_call(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t vstart,
+                          uint64_t pstart, uint64_t op, uint64_t cap, uint64_t tail) {
+    if constexpr (E::kInlineBlocks) {
+        return block<kRing>(em, w, in, n, out, vstart, pstart, op, cap, tail);
+    } else if constexpr (!kRing) {
+        return block_noinline<false>(em, w, in, n, out, vstart, pstart, op, cap, tail);
+    } else {
+        if (vstart == pstart) return block_noinline<false>(em, w, in, n, out, vstart, pstart, op, cap, tail);
+        return block_noinline<true>(em, w, in, n, out, vstart, pstart, op, cap, tail);
+    }
 }
 
 // ------------------------------------------------------------------ XXH64
@@ -1231,8 +1277,10 @@ RPC_HD bool adapt(Bufs& s, uint64_t need_in, uint64_t need_out) {
 
 // One call of the wrapper over one buffer.  out[0, cap) is the output slot.
 // Returns a verdict; *out_len = bytes produced.  `cap` too small for what the
-// library would produce -> V_OVERFLOW.
-template <class E, class W>
+// library would produce -> V_OVERFLOW.  kRing false: V_RING where a ring
+// wraps (the lane decoder's first pass: the ring's history cost it registers,
+// 704 vs 586 ms per C4 step, although C4's frames never wrap).
+template <bool kRing, class E, class W>
 RPC_HD int32_t uncompress_impl(E& em, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len,
                                W& w) {
     uint64_t T = 0, p = 0;
@@ -1283,7 +1331,7 @@ RPC_HD int32_t uncompress_impl(E& em, const uint8_t* in, uint64_t n, uint8_t* ou
                 if (type == 2) {
                     if (T > cap) return V_OVERFLOW;
                     const uint64_t lim = fend < cap ? fend : cap;
-                    r = block_call(em, w, f + ip, size, out, fstart, T, lim - T, cap);
+                    r = block_call<kRing>(em, w, f + ip, size, out, fstart, fstart, T, lim - T, cap);
                     if (r == -2 || (r < 0 && lim < fend)) return fend <= cap ? V_ERROR : V_OVERFLOW;
                     if (r < 0) return RPZ_FAIL(V_ERROR);
                     ip += size;
@@ -1322,6 +1370,7 @@ RPC_HD int32_t uncompress_impl(E& em, const uint8_t* in, uint64_t n, uint8_t* ou
             if (!adapt(bufs, need_in, need_out)) return RPZ_FAIL(V_ERROR);  // memory_allocation: runtime_error
         }
         uint64_t decoded = 0, ostart = 0;
+        w.ring_v = w.ring_p = fstart;
         bool done = false;
         for (;;) {
             if (rem - ip < 3) break;  // partial block header
@@ -1364,7 +1413,7 @@ RPC_HD int32_t uncompress_impl(E& em, const uint8_t* in, uint64_t n, uint8_t* ou
                     if (avail < size) break;  // waits in the load stage
                     if (T > cap) return V_OVERFLOW;
                     const uint64_t lim = room_ring < cap - T ? room_ring : cap - T;
-                    const int64_t rr = block_call(em, w, f + ip, size, out, fstart, T, lim, cap);
+                    const int64_t rr = block_call<kRing>(em, w, f + ip, size, out, w.ring_v, w.ring_p, T, lim, cap);
                     if (rr == -2 || (rr < 0 && lim < room_ring)) {
                         // the slot, not the library, ran out: decide with the bound
                         return V_OVERFLOW;
@@ -1405,7 +1454,12 @@ RPC_HD int32_t uncompress_impl(E& em, const uint8_t* in, uint64_t n, uint8_t* ou
                 done = true;
                 break;
             }
-            if (r && bufs.out < h.fcs && ostart + h.bsm > bufs.out) ostart = 0;  // ring wraps
+            if (r && bufs.out < h.fcs && ostart + h.bsm > bufs.out) {  // ring wraps
+                if constexpr (!kRing) return V_RING;
+                ostart = 0;
+                w.ring_v = w.ring_p;
+                w.ring_p = T;
+            }
         }
         if (!done) {  // input ended inside the frame: what was decoded stands
             *out_len = T;
@@ -1474,12 +1528,13 @@ RPC_HD uint64_t bound(const uint8_t* in, uint64_t n) {
     return b;
 }
 
-template <class E, class W>
+template <bool kRing = true, class E, class W>
 RPC_HD int32_t uncompress(E& em, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len, W& w) {
     *out_len = 0;
     if (n == 0) return RPZ_FAIL(V_ERROR);  // "Asked to stream_zstd::uncompress empty buffer"
-    const int32_t v = uncompress_impl(em, in, n, out, cap, out_len, w);
+    const int32_t v = uncompress_impl<kRing>(em, in, n, out, cap, out_len, w);
     em.sync();
+    if (v == V_RING) return v;
     if (v == V_OVERFLOW && bound(in, n) <= cap) return RPZ_FAIL(V_ERROR);
     return v;
 }

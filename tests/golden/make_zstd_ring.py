@@ -1,0 +1,42 @@
+"""Fixture generator (run here, not on the GPU box): crafted zstd frames whose
+1 KiB window makes the reference loop's ring buffer wrap every two blocks,
+each with one match whose offset reaches into the previous ring segment
+(where the current one has or has not overwritten it) or before it
+(corruption_detected in libzstd).  Made by tests/native/zstd_fuzz.cpp
+--dump-ring (the engine's own zstd encoder pieces, predefined FSE tables);
+the expected outputs come from the oracle (libzstd 1.4.9 through
+stream_zstd::do_uncompress) at test time.  Writes tests/golden/zstd_ring.npz."""
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+# (offset, blocks, bad block): small frames for the lane decoder, ~300 KiB ones
+# (their bound is 1 KiB per block) for the wave decoder
+CASES = [(900, 8, 5), (1500, 8, 5), (2100, 8, 5), (2600, 8, 5), (3000, 8, 5), (3152, 8, 5), (3153, 8, 5),
+         (5200, 8, 5), (700, 9, 8), (2500, 12, 11), (2600, 300, 201), (3153, 300, 201)]
+
+
+def main():
+    from test_zstd_fuzz import build_fuzzer
+
+    with tempfile.TemporaryDirectory() as tmp:
+        exe = build_fuzzer(Path(tmp))
+        frames = []
+        for off, nb, bad in CASES:
+            subprocess.run([str(exe), "--seed", "11", "--dump-ring", f"{off},{nb},{bad}"], cwd=tmp, check=True)
+            frames.append(np.frombuffer((Path(tmp) / "ring.zst").read_bytes(), dtype=np.uint8))
+    lens = np.array([len(f) for f in frames], dtype=np.int64)
+    np.savez_compressed(ROOT / "tests" / "golden" / "zstd_ring.npz", data=np.concatenate(frames), lens=lens,
+                        cases=np.array(CASES, dtype=np.int64))
+    print("wrote", len(frames), "frames,", int(lens.sum()), "bytes")
+
+
+if __name__ == "__main__":
+    main()

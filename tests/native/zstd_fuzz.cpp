@@ -24,6 +24,7 @@
 
 #include "rpgpu.h"
 #include "rpgpu_zstd.h"
+#include "rpgpu_zstdc.h"
 
 extern "C" {
 int32_t orc_uncompress(int codec, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
@@ -39,7 +40,7 @@ namespace {
 typedef std::vector<uint8_t> Bytes;
 std::mt19937_64 rng;
 uint64_t below(uint64_t n) { return n ? rng() % n : 0; }
-long n_cases = 0, n_ok = 0, n_rejected = 0;
+long n_cases = 0, n_ok = 0, n_rejected = 0, n_ring = 0;
 
 void fail(const char* what) {
     fprintf(stderr, "FAIL: %s\n", what);
@@ -295,7 +296,13 @@ void compare(const Bytes& in) {
     static rpzstd::Ws ws;
     uint64_t elen = 0;
     rpzstd::DirectEmit em;
-    const int32_t ev = rpzstd::uncompress(em, ip, in.size(), eout.data(), cap, &elen, ws);
+    // as the device does: the lane pass (no ring history), then the ring pass
+    // for a body whose ring wrapped (rpgpu_decomp.hip zstd_ring_kernel)
+    int32_t ev = rpzstd::uncompress<false>(em, ip, in.size(), eout.data(), cap, &elen, ws);
+    if (ev == rpzstd::V_RING) {
+        n_ring++;
+        ev = rpzstd::uncompress<true>(em, ip, in.size(), eout.data(), cap, &elen, ws);
+    }
     static Bytes oout(96u << 20);
     size_t olen = 0;
     const int32_t ov = orc_uncompress(4, ip, in.size(), oout.data(), oout.size(), &olen);
@@ -374,6 +381,142 @@ void check_windows() {
     }
 }
 
+// streaming frames whose ring buffer wraps many times (windows of 1-4 KiB, no
+// content size: ring = window + block + 64) with corrupt offsets in them: the
+// ring's extDict view (ZSTD_checkContinuity / ZSTD_execSequence), where a
+// flat history would accept offsets libzstd rejects or read other bytes
+Bytes ring_frame() {
+    ZSTD_CCtx* c = ZSTD_createCCtx();
+    const int levels[] = {1, 3, 3, 9, 19};
+    ck(ZSTD_CCtx_setParameter(c, ZSTD_c_compressionLevel, levels[below(5)]));
+    ck(ZSTD_CCtx_setParameter(c, ZSTD_c_windowLog, 10 + (int)below(3)));
+    ck(ZSTD_CCtx_setParameter(c, ZSTD_c_contentSizeFlag, 0));
+    ck(ZSTD_CCtx_setParameter(c, ZSTD_c_checksumFlag, below(3) == 0));
+    const Bytes src = payload(20000 + below(120000));
+    Bytes out(ZSTD_compressBound(src.size()) + 64);
+    const size_t r = ZSTD_compress2(c, out.data(), out.size(), src.data(), src.size());
+    ck(r);
+    out.resize(r);
+    ZSTD_freeCCtx(c);
+    return out;
+}
+
+// One compressed block: raw literals, then the given sequences with the
+// predefined FSE tables (the bitstream written last-first as
+// ZSTD_encodeSequences does; rpgpu_zstdc.h's encoder pieces).
+Bytes seq_block(const Bytes& lits, const std::vector<rpzstdc::Seq>& seqs) {
+    static rpzstdc::Ws w;
+    static bool init = false;
+    if (!init) rpzstdc::init_tables(w), init = true;
+    Bytes out(lits.size() + 64 + 16 * seqs.size());
+    const uint32_t nlit = (uint32_t)lits.size();
+    out[0] = (uint8_t)((3u << 2) | ((nlit & 15) << 4));  // raw, 20-bit size
+    out[1] = (uint8_t)(nlit >> 4);
+    out[2] = (uint8_t)(nlit >> 12);
+    uint64_t o = 3;
+    for (uint8_t c : lits) out[o++] = c;
+    const uint32_t nseq = (uint32_t)seqs.size();
+    out[o++] = (uint8_t)nseq;  // < 128
+    out[o++] = 0;              // LL, OF, ML: predefined
+    rpzstdc::BitW b{out.data(), o, 0, 0};
+    rpzstdc::CState sll, sof, sml;
+    const rpzstdc::Seq& last = seqs[nseq - 1];
+    uint32_t llc = rpzstdc::ll_code(last.ll), mlc = rpzstdc::ml_code(last.ml), ofv = last.off + 3,
+             ofc = rpzstdc::hb32(ofv);
+    rpzstdc::init_state(sml, w.ml, mlc);
+    rpzstdc::init_state(sof, w.of, ofc);
+    rpzstdc::init_state(sll, w.ll, llc);
+    b.add(last.ll - rpzstd::kLLBase[llc], rpzstd::kLLBits[llc]);
+    b.add(last.ml - rpzstd::kMLBase[mlc], rpzstd::kMLBits[mlc]);
+    b.add(ofv, ofc);
+    for (uint32_t k = nseq - 1; k-- > 0;) {
+        const rpzstdc::Seq& q = seqs[k];
+        llc = rpzstdc::ll_code(q.ll), mlc = rpzstdc::ml_code(q.ml), ofv = q.off + 3, ofc = rpzstdc::hb32(ofv);
+        rpzstdc::encode_sym(b, sof, w.of, ofc);
+        rpzstdc::encode_sym(b, sml, w.ml, mlc);
+        rpzstdc::encode_sym(b, sll, w.ll, llc);
+        b.add(q.ll - rpzstd::kLLBase[llc], rpzstd::kLLBits[llc]);
+        b.add(q.ml - rpzstd::kMLBase[mlc], rpzstd::kMLBits[mlc]);
+        b.add(ofv, ofc);
+    }
+    b.add(sml.value, w.ml.log);
+    b.add(sof.value, w.of.log);
+    b.add(sll.value, w.ll.log);
+    b.close();
+    out.resize(b.o);
+    return out;
+}
+
+// A 1 KiB-window frame without content size: ring = 2,112 bytes, so the ring
+// wraps every two 1,024-byte blocks (segments [0, 2048), [2048, 4096), ...).
+// Block `bad` (>= 4) carries one sequence whose offset reaches back `off`
+// bytes from 80 bytes into the block: into the previous segment where the
+// current one has or has not overwritten it, to its very start, or before it
+// (corruption_detected in libzstd; a flat history would accept it).
+Bytes crafted_ring_frame(int nblocks, int bad, uint32_t off) {
+    Bytes f = {0x28, 0xB5, 0x2F, 0xFD, 0x00, 0x00};  // no FCS / checksum; window 1 KiB
+    for (int k = 0; k < nblocks; k++) {
+        Bytes lits;
+        std::vector<rpzstdc::Seq> seqs;
+        if (k == bad) {
+            for (int j = 0; j < 984; j++) lits.push_back((uint8_t)('a' + (rng() % 16)));
+            seqs.push_back(rpzstdc::Seq{80, 40, off});  // then 904 trailing literals
+        } else {
+            for (int j = 0; j < 1000; j++) lits.push_back((uint8_t)('A' + (rng() % 16)));
+            seqs.push_back(rpzstdc::Seq{900, 24, 1 + (uint32_t)below(k == 0 ? 899 : 1000)});
+        }
+        const Bytes blk = seq_block(lits, seqs);
+        const uint32_t last = k + 1 == nblocks ? 1u : 0u;
+        const uint32_t bh = last | (2u << 1) | ((uint32_t)blk.size() << 3);
+        f.push_back((uint8_t)bh), f.push_back((uint8_t)(bh >> 8)), f.push_back((uint8_t)(bh >> 16));
+        f.insert(f.end(), blk.begin(), blk.end());
+    }
+    return f;
+}
+
+// Not restated: libzstd's wildcopy over-writes (literal and match copies
+// write up to 32-48 bytes past their end, into the ring) -- an offset that
+// reads the extDict within 64 bytes past the current write position reads
+// those bytes.  Such offsets lie beyond the window; matches reading any
+// extDict byte there are skipped here.
+bool in_overrun_band(int bad, uint32_t off) {
+    const uint64_t lit_end = (uint64_t)bad * 1024 + 80, pstart = (uint64_t)(bad / 2) * 2048;
+    if (bad < 2 || off <= lit_end - pstart || off > lit_end - (pstart - 2048)) return false;
+    const uint64_t a = lit_end - off - (pstart - 2048), lw = lit_end - pstart;
+    const uint64_t len1 = pstart - (lit_end - off), n = len1 < 40 ? len1 : 40;  // extDict bytes read
+    return a < lw + 64 && a + n > lw;
+}
+
+void check_ring_crafted() {
+    // bad block 5: flat [5120, 6144), segment [4096, 6144), extDict [2048, 4096);
+    // the match starts at 5200: the current segment has written ring [0, 1104)
+    for (uint32_t off : {900u, 1104u, 1500u, 2000u, 2100u, 2600u, 3000u, 3100u, 3152u, 3153u, 3500u, 5000u, 5200u})
+        for (int rep = 0; rep < 3; rep++) compare(crafted_ring_frame(8, 5, off));
+    for (int i = 0; i < 300; i++) {
+        const int bad = 2 + (int)below(9);
+        const uint32_t off = 1 + (uint32_t)below(1024u * (uint32_t)(bad + 1));
+        if (in_overrun_band(bad, off)) continue;
+        compare(crafted_ring_frame(bad + 1 + (int)below(3), bad, off));
+    }
+}
+
+void check_ring(long cases) {
+    for (long i = 0; i < cases; i++) {
+        const Bytes f = ring_frame();
+        compare(f);
+        if (f.size() <= 16) continue;
+        for (int k = 0; k < 12; k++) {
+            Bytes g = f;
+            for (int j = 0, flips = 1 + (int)below(3); j < flips; j++) {
+                const size_t at = 8 + below(g.size() - 8);
+                if (below(2)) g[at] ^= (uint8_t)(1u << below(8));
+                else g[at] = (uint8_t)rng();
+            }
+            compare(g);
+        }
+    }
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -385,6 +528,16 @@ int main(int argc, char** argv) {
         if (!strcmp(argv[a], "--seed")) seed = strtoull(argv[a + 1], nullptr, 0);
         if (!strcmp(argv[a], "--replay")) replay = argv[a + 1];
         if (!strcmp(argv[a], "--exact")) g_exact = atoi(argv[a + 1]) != 0;
+        if (!strcmp(argv[a], "--dump-ring")) {  // OFF[,BLOCKS,BAD]: a crafted ring frame to ring.zst
+            rng.seed(seed);
+            unsigned off = 0, nb = 8, bad = 5;
+            if (sscanf(argv[a + 1], "%u,%u,%u", &off, &nb, &bad) < 1 || bad >= nb) return 2;
+            const Bytes f = crafted_ring_frame((int)nb, (int)bad, off);
+            FILE* fp = fopen("ring.zst", "wb");
+            if (!fp || fwrite(f.data(), 1, f.size(), fp) != f.size()) return 2;
+            fclose(fp);
+            return 0;
+        }
     }
     rng.seed(seed);
     if (replay) {
@@ -400,6 +553,8 @@ int main(int argc, char** argv) {
     }
     check_select();
     check_windows();
+    check_ring_crafted();
+    check_ring(cases / 8 + 1);
     check_ncount(cases * 4);
     for (long i = 0; i < cases; i++) {
         Bytes b = body();
@@ -411,6 +566,7 @@ int main(int argc, char** argv) {
             compare(c);
         }
     }
-    printf("zstd fuzz: %ld cases, %ld decoded, %ld rejected: engine == oracle\n", n_cases, n_ok, n_rejected);
+    printf("zstd fuzz: %ld cases (%ld through the ring pass), %ld decoded, %ld rejected: engine == oracle\n",
+           n_cases, n_ring, n_ok, n_rejected);
     return 0;
 }

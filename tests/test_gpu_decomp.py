@@ -466,3 +466,24 @@ def test_mutated_payloads_many(eng, codec):
     bs = [batch(c, fmt=WIRE, record_count=rc, attrs=codec) for c, rc in mutated_bodies(rng, codec, 600)]
     data, descs = arena(bs, fmt=WIRE, ops=OPS)
     compare(eng.decompress_arena(data, descs), data, descs)
+
+
+def test_zstd_ring_extdict_frames(eng):
+    """Crafted zstd frames (tests/golden/make_zstd_ring.py) whose 1 KiB window
+    makes the reference loop's ring buffer wrap every two blocks, each with one
+    match reaching into the previous ring segment -- where the current segment
+    has or has not overwritten it -- or before it (libzstd: corruption_detected):
+    8 KiB frames on the lane decoder, ~300 KiB ones on the wave decoder.  Every
+    verdict, length and byte as the oracle's (libzstd 1.4.9 through
+    stream_zstd::do_uncompress)."""
+    from redpanda_amd import abi
+
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "zstd_ring.npz"))
+    ends = np.cumsum(g["lens"])
+    frames = [g["data"][e - n:e].tobytes() for e, n in zip(ends, g["lens"])]
+    bs = [batch(f, fmt=WIRE, record_count=1, attrs=4) for f in frames]
+    data, descs = arena(bs, fmt=WIRE, ops=OPS)
+    got = eng.decompress_arena(data, descs)
+    want = compare(got, data, descs)
+    v = want["verdicts"]
+    assert (v == abi.V_OK).sum() >= 6 and (v == abi.V_DECOMP_ERROR).sum() >= 2, v
