@@ -158,7 +158,11 @@ hipError_t launch_summaries(const rpgpu_batch_desc* d_descs, const rpgpu_batch_r
     if (nparts == 0) return hipSuccess;
     if (d_partial && nparts <= kLdsParts && n > 0) {
         // enough batches per workgroup to amortise its table (>= 4 per partition)
-        uint32_t g = (uint32_t)(((uint64_t)n + 4ull * nparts - 1) / (4ull * nparts));
+#ifndef RPGPU_SUM_PER_PART
+#define RPGPU_SUM_PER_PART 4
+#endif
+        uint32_t g = (uint32_t)(((uint64_t)n + (uint64_t)RPGPU_SUM_PER_PART * nparts - 1) /
+                                ((uint64_t)RPGPU_SUM_PER_PART * nparts));
         if (g > summary_groups(cu_count)) g = summary_groups(cu_count);
         if (g < 1) g = 1;
         summary_lds_kernel<<<g, kSumThreads, 0, s>>>(d_descs, d_res, n, part_lo, nparts, d_partial);
