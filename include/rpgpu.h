@@ -702,7 +702,14 @@ int32_t rpgpu_partition_summaries_device(rpgpu_ctx* ctx, const rpgpu_batch_desc*
  * their memory budgets (spill_key_index.cc:99-138; compaction_key_reducer,
  * compaction_reducers.cc:49-67).  Past them the reference evicts entries in
  * its hash map's iteration order and keeps the evicted keys' records as well,
- * which this engine does not reproduce (it can only keep fewer records).
+ * which this engine does not reproduce (it can only keep fewer records).  That
+ * order is not a function of the input: the map is an absl::node_hash_map, and
+ * absl's SwissTable starts each probe at H1 = (hash >> 7) ^ PerTableSalt(ctrl),
+ * a salt taken from the address of the table's control bytes, so which entry
+ * is "first" depends on where the heap put the table.  A caller wanting the
+ * reference's bytes sends a scope whose distinct keys (*d_nkeys for a one-scope
+ * call) would exceed the budget (5 MiB: ~60 B of map per key plus its bytes)
+ * to the reference's CPU path.
  * d_scratch: rpgpu_compaction_scratch_bytes(index_cap) bytes. */
 size_t rpgpu_compaction_scratch_bytes(uint64_t index_cap);
 int32_t rpgpu_compaction_keep_device(rpgpu_ctx* ctx, const uint8_t* d_data, const rpgpu_batch_desc* d_descs,
