@@ -155,9 +155,12 @@ constexpr uint64_t kLaneMaxSlot = 256u << 10;
 constexpr uint64_t kZstdLaneMaxSlot = RPGPU_ZSTD_LANE_MAX;  // zstd: its lane / wave boundary
 __device__ __forceinline__ uint64_t lane_max(uint32_t codec) { return codec == 4 ? kZstdLaneMaxSlot : kLaneMaxSlot; }
 // LZ4 / snappy-java slots above this are split into parts when the frame allows
-// (at most kLaneMaxSlot: the lane decoders take the unsplit ones below it)
+// (at most kLaneMaxSlot: the lane decoders take the unsplit ones below it).
+// 80 KiB: a 64 KiB block (C3) stays one lane's; bigger frames no longer leave a
+// lane decoding up to 256 KiB as the launch's tail (C5 424.2 / 425.1 vs 437.1 /
+// 433.6 ms at 256 KiB, 425.4 / 426.4 at 128 KiB; C3 77.17 either way)
 #ifndef RPGPU_SPLIT_MIN
-#define RPGPU_SPLIT_MIN (256u << 10)
+#define RPGPU_SPLIT_MIN (80u << 10)
 #endif
 constexpr uint64_t kSplitMinSlot = RPGPU_SPLIT_MIN;
 static_assert(kSplitMinSlot <= kLaneMaxSlot, "split threshold above the lane decoders' limit");
