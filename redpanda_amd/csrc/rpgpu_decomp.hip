@@ -618,8 +618,10 @@ __global__ __launch_bounds__(64) void decomp_wave_kernel(
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
         uint64_t sz = slot[i];
-        // the large batches of this instance's codec family; the lane kernels take the rest
-        if (!wave_owned(d, v, sz) || !in_family(FAM, v.codec)) continue;
+        // the listed batches: this family's large ones (decomp_caps_kernel) and, for LZ,
+        // split bodies whose parts did not bear the plan out (split_finish_kernel) --
+        // those may be as small as the split threshold, below the wave size
+        if (!decomp_wanted(d, v) || !in_family(FAM, v.codec)) continue;
         const uint64_t off = block_base[i / kScanBlock] + local[i];
         int32_t verdict = RPGPU_V_SKIPPED;
         uint64_t len = 0;

@@ -487,3 +487,23 @@ def test_zstd_ring_extdict_frames(eng):
     want = compare(got, data, descs)
     v = want["verdicts"]
     assert (v == abi.V_OK).sum() >= 6 and (v == abi.V_DECOMP_ERROR).sum() >= 2, v
+
+
+def test_split_fallback_below_wave_size(eng):
+    """A corrupt LZ4 frame from C5's arena (batch 126,469 of the bench's seed,
+    tests/golden/lz4_split_fallback.npz: 45,806 bytes, two 64 KiB blocks, the
+    first decoding to 65,534 bytes) is split (slot above the 80 KiB split
+    threshold), its parts do not bear the plan out, and the serial fallback --
+    the LZ wave decoder, for a batch below the wave size -- gives the serial
+    verdict (DECOMP_ERROR), as the oracle does.  Round 4's first 80 KiB build
+    left such batches undecoded."""
+    from redpanda_amd import abi
+
+    body = np.load(os.path.join(os.path.dirname(__file__), "golden", "lz4_split_fallback.npz"))["body"].tobytes()
+    rng = np.random.default_rng(3)
+    good = orc.compress(3, b"".join(records(rng, 40, 4, 3000, text=True)))
+    bs = [batch(body, fmt=WIRE, record_count=64, attrs=3), batch(good, fmt=WIRE, record_count=40, attrs=3)]
+    data, descs = arena(bs, fmt=WIRE, ops=OPS)
+    got = eng.decompress_arena(data, descs)
+    want = compare(got, data, descs)
+    assert want["verdicts"][0] == abi.V_DECOMP_ERROR and want["verdicts"][1] == abi.V_OK
