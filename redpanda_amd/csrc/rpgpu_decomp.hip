@@ -794,22 +794,23 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
         if ((e = hipStreamWaitEvent(ds->aux, ds->fork, 0)) != hipSuccess) return e;
         ws = ds->aux;
     }
-    // split batches: LZ4 parts ahead of the lane kernels on the main stream,
-    // snappy parts on the second, then their verdicts there (failures join
-    // the LZ wave list); the two streams' chains come out about even
+    // split batches: LZ4 and snappy parts ahead of the lane kernels on the main
+    // stream, then their verdicts on the second, after its zstd wave decoder
+    // (failures join the LZ wave list).  With bodies split above 80 KiB the
+    // main stream's lane launches got shorter and the snappy parts moved over
+    // from the second stream, which the zstd wave decoder keeps the longer one.
     const uint32_t pgrid = (part_cap(n) / 2 < 65536u ? part_cap(n) / 2 + 255 : 65536u + 255) / 256;
     part_kernel<3><<<pgrid, 256, 0, s>>>(p.parts, p.counter + 4, part_cap(n), d_descs, d_data, p.slot, p.local,
+                                         p.block_sum, d_out, out_cap, p.pres);
+    part_kernel<2><<<pgrid, 256, 0, s>>>(p.parts, p.counter + 5, part_cap(n), d_descs, d_data, p.slot, p.local,
                                          p.block_sum, d_out, out_cap, p.pres);
     if (ds) {
         if ((e = hipEventRecord(ds->parts, s)) != hipSuccess) return e;
     }
-    // zstd frames above kZstdLaneMaxSlot first on the second stream (the wave
-    // decoder), then the snappy parts there
+    // zstd frames above kZstdLaneMaxSlot on the second stream (the wave decoder)
     decomp_wave_kernel<kFamZstd><<<decomp_waves(n), 64, sizeof(rpzstd::Ws), ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
                                                                 p.block_sum, d_dres, d_out, out_cap, d_out_descs,
                                                                 p.counter + 1, p.lits, p.wlist, p.counter + 2);
-    part_kernel<2><<<pgrid, 256, 0, ws>>>(p.parts, p.counter + 5, part_cap(n), d_descs, d_data, p.slot, p.local,
-                                          p.block_sum, d_out, out_cap, p.pres);
     if (ds) {
         if ((e = hipStreamWaitEvent(ws, ds->parts, 0)) != hipSuccess) return e;
     }
