@@ -24,6 +24,12 @@ already resident in HBM, then the final gather of per-partition summaries.
 Multi-GPU: one process per GPU (torch.distributed over RCCL).  Each rank owns
 a contiguous partition range (redpanda_amd/shard.py) and touches only its
 own batches; the one exchange is the all-gather of per-partition summaries.
+Under torchrun (WORLD_SIZE set) this process is one rank; `--gpus N` without
+it starts the N rank processes itself (launch_ranks), before anything here
+touches the GPU, and returns the worst of their exit codes.  `--dry-run`
+runs the same launcher / rendezvous / sharding / gather path on the CPU over
+gloo without the engine (the summaries count the descriptors only), for
+tests/test_bench_launch.py.
 
 The CPU baseline is the oracle (the C restatement of the reference path: SSE4.2
 CRC32C, liblz4 / libzstd / snappy through the reference's wrapper loops) on
@@ -217,6 +223,80 @@ def full_check(spec, chunks, part_shift, res, dres, ores, index, gen_threads, pi
                                         for v, n_ in zip(*np.unique(res["verdict"], return_counts=True))}}
 
 
+# ---- rank launcher (--gpus N without torchrun) -------------------------------------------
+def launch_ranks(nranks: int, argv: list[str]) -> int:
+    """Start `nranks` copies of this script as ranks 0..N-1 of one job (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, rendezvous on
+    127.0.0.1), wait for all of them and return the worst exit code.  The
+    parent never touches the GPU (no torch import here): the ranks are fresh
+    child processes, not an exec of this one.  Rank 0 alone prints the JSON
+    line, on the inherited stdout.  If a rank fails, the others are stopped
+    (by their own PIDs) so the job cannot hang in a collective."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(nranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nranks),
+                   LOCAL_WORLD_SIZE=str(nranks), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    worst = 0
+    pending = list(procs)
+    while pending:
+        time.sleep(0.2)
+        for p in list(pending):
+            rc = p.poll()
+            if rc is None:
+                continue
+            pending.remove(p)
+            if rc != 0:
+                worst = worst or rc
+                log(f"[launcher] rank {procs.index(p)} exited with {rc}; stopping the others")
+                for q in pending:
+                    q.terminate()
+                for q in pending:
+                    try:
+                        q.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                pending = []
+    return worst
+
+
+def descriptor_summaries(descs, lo: int, hi: int):
+    """--dry-run's per-partition summaries: batches and wire bytes per partition
+    from the descriptors alone (no validation runs on the dry path)."""
+    import torch
+
+    from redpanda_amd import shard
+
+    out = torch.zeros(hi - lo, shard.NF, dtype=torch.int64)
+    part = torch.from_numpy(descs["partition"].astype(np.int64)) - lo
+    out[:, 0].index_add_(0, part, torch.ones(len(descs), dtype=torch.int64))
+    out[:, 3].index_add_(0, part, torch.from_numpy(descs["length"].astype(np.int64)))
+    out[:, 5] = -1
+    return out
+
+
+def rank_coverage(table, world: int, partitions: int, expect_batches: int) -> dict:
+    """Which ranks' partition ranges came back from the gather with batches in
+    them, and whether the gathered batch count is the job's."""
+    from redpanda_amd import shard
+
+    t = table.cpu().numpy()
+    present = [g for g in range(world)
+               if t[slice(*shard.partition_range(g, world, partitions)), 0].sum() > 0]
+    got = int(t[:, 0].sum())
+    return {"ranks_present": present, "gathered_batches": got, "expected_batches": expect_batches,
+            "all_ranks_present": present == list(range(world)) and got == expect_batches}
+
+
 # ---- the workload of one rank ------------------------------------------------------------
 def rank_chunks(cfg: dict, rank: int, world: int, scaling: str, n_override: int):
     """[(first_batch_id, count)] of the batches this rank owns, the global
@@ -234,6 +314,44 @@ def rank_chunks(cfg: dict, rank: int, world: int, scaling: str, n_override: int)
     n = n_override or cfg["batches"]
     first = rank * n
     return [(first, n)], world * P, rank * P, (rank * P, (rank + 1) * P)
+
+
+def dry_run(args, cfg: dict, world: int, rank: int) -> int:
+    """The multi-rank skeleton of main() on the CPU over gloo: each rank takes its
+    partition range (rank_chunks), generates its batches' descriptors, reduces them
+    to per-partition summaries and joins the all-gather; rank 0 prints a JSON line
+    with `n_gpus` and the gather's rank coverage.  No engine call, so no throughput."""
+    import torch
+    import torch.distributed as dist
+
+    from redpanda_amd import abi, engine, shard
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    scaling = args.scaling or cfg.get("default_scaling", "weak")
+    spec = engine.make_spec(seed=0x5EED0000 + int(args.config[1:]), partitions=cfg["partitions"], **cfg["spec"])
+    chunks, P_total, part_shift, (plo, phi) = rank_chunks(cfg, rank, world, scaling, args.batches)
+    parts = []
+    for first, m in chunks:
+        _, d = engine.build_arena(spec, m, first=first, nthreads=1)
+        d["partition"] += part_shift
+        parts.append(d)
+    descs = np.concatenate(parts) if parts else np.zeros(0, dtype=abi.DESC_DTYPE)
+    assert ((descs["partition"] >= plo) & (descs["partition"] < phi)).all(), "batch outside the rank's range"
+    table = shard.gather_summaries(descriptor_summaries(descs, plo, phi), world, P_total)
+    n_all = torch.tensor([len(descs)], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(n_all)
+    cov = rank_coverage(table, world, P_total, int(n_all.item()))
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "dry_run": True,
+                          "scaling": scaling, "config": {"workload": cfg["workload"], "batches_per_rank0": len(descs),
+                                                          "partitions_total": P_total,
+                                                          "parallelism": f"partition-shard x{world}"},
+                          "gather": cov}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if cov["all_ranks_present"] else 3
 
 
 def main() -> int:
@@ -257,7 +375,12 @@ def main() -> int:
                     help="the record walk beside the checksums (auto: the library default, on; "
                          "off: RPGPU_OPT_NO_WALK_OVERLAP)")
     ap.add_argument("--blocks-per-cu", type=int, default=0, help="rpgpu_opts.blocks_per_cu (tuning; 0 = default)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU only: launcher, gloo rendezvous, sharding and the summary gather, no engine")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])
 
     import torch
     import torch.distributed as dist
@@ -267,12 +390,16 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    cfg = CONFIGS[args.config]
+    if args.dry_run:
+        return dry_run(args, cfg, world, rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    cfg = CONFIGS[args.config]
     scaling = args.scaling or cfg.get("default_scaling", "weak")
     decompress = bool(cfg.get("decompress"))
     gen_threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
@@ -412,11 +539,13 @@ def main() -> int:
     res = d_res.cpu().numpy().view(abi.RESULT_DTYPE)
     summary = table[0].cpu().numpy()
     wire = float(descs["length"].astype(np.float64).sum())
-    wire_all = wire
+    wire_all, n_job = wire, n
     if world > 1:
-        t = torch.tensor([wire], dtype=torch.float64, device=dev)
+        t = torch.tensor([wire, float(n)], dtype=torch.float64, device=dev)
         dist.all_reduce(t)
-        wire_all = float(t.item())
+        wire_all, n_job = float(t[0].item()), int(t[1].item())
+    # the gather must hold every rank's partition range and every batch of the job
+    coverage = rank_coverage(table[0], world, P_total, n_job)
     ok_in = int(summary[:, 1].sum())
     n_all = int(summary[:, 0].sum())
     if decompress:
@@ -451,6 +580,7 @@ def main() -> int:
         "algorithmic_gbps_per_gpu": round(alg_bytes * args.steps / elapsed / 1e9, 2),
         "verdicts_rank0": hist,
         "batches_ok_all_ranks": ok_in,
+        "gather": coverage,
         "h2d_gbps_pinned": round(h2d_bytes / max(h2d_time, 1e-9) / 1e9, 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
@@ -482,7 +612,11 @@ def main() -> int:
             pass
 
     # ---- CPU baseline: the oracle on this host's cores, bounded sample -----------------
-    if rank == 0 and not args.no_cpu_baseline:
+    # the CPU baseline is timed on rank 0 at N=1 only (the other ranks would sit in
+    # the job's teardown while it runs, and the host cores are shared by N ranks)
+    if world > 1:
+        out["cpu_baseline_note"] = "timed at --gpus 1 only"
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import oracle.oracle as orc
 
         T, hostinfo = effective_cores()
