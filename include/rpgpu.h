@@ -214,13 +214,12 @@ typedef struct rpgpu_opts {
      * (minimum 256) bounds the memory: the batches still decode, each lane
      * taking more of them. */
     uint32_t decomp_ws_lanes;
-    /* the walk overlap: k > 1 = the arena checksummed in k chunks, each
-     * chunk's walk beside the next chunk's checksums (0 = 16; at most 256);
-     * 1 = checksums and speculative record walks side by side over the whole
-     * arena, one launch each (slower on C2: 4.97 vs 4.26 ms per step). */
+    /* the walk overlap: the arena checksummed in k chunks, each chunk's walk
+     * beside the next chunk's checksums (0 = 16; at most 256; 1 = one
+     * checksum launch, then the walk). */
     uint16_t walk_chunks;
     /* validate_kernel workgroups per CU of the persistent grid (0 = 8,
-     * capped by occupancy; 5 beside a side-by-side walk; at most 32). */
+     * capped by occupancy; at most 32). */
     uint16_t blocks_per_cu;
 } rpgpu_opts;
 #define RPGPU_DEFAULT_MAX_DECODED_BATCH (64ull << 20)

@@ -222,14 +222,10 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
         delete c;
         return nullptr;
     }
-    // the walk overlap: chunked (the default, 16 chunks) or checksums and
-    // walks side by side (walk_chunks 1): C2 4.26 vs 4.97 / 4.50 ms per step
-    // (5 / 6 checksum workgroups per CU, profiles/r4/NOTES.md r4b)
+    // the walk overlap: the arena checksummed in 16 chunks, each chunk's walk beside
+    // the next chunk's checksums (20 / 24 / 32 chunks measured slower, profiles/r4/NOTES.md)
     c->overlap.chunks = 16;
     if (opts && opts->walk_chunks >= 1 && opts->walk_chunks <= rpgpu::kMaxRunChunks) c->overlap.chunks = opts->walk_chunks;
-    // side by side, the checksum grid leaves each SIMD room for a walk wave
-    c->overlap.grid = c->cu_count * (opts && opts->blocks_per_cu ? (int)opts->blocks_per_cu : rpgpu::kSideBlocksPerCU);
-    if (c->overlap.grid > c->grid) c->overlap.grid = c->grid;
     c->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     c->have_dstreams = hipStreamCreateWithFlags(&c->dstreams.aux, hipStreamNonBlocking) == hipSuccess &&
                        hipEventCreateWithFlags(&c->dstreams.fork, hipEventDisableTiming) == hipSuccess &&

@@ -33,9 +33,6 @@ static_assert(kTableWords % 4 == 0, "table blob is copied as 16-byte words");
 constexpr int kValidateThreads = 256;  // 4 waves per workgroup
 constexpr int kWavesPerBlock = kValidateThreads / 64;
 constexpr int kBlocksPerCU = 8;  // default grid: workgroups of 4 waves per CU
-// checksum grid beside the concurrent walk: 5 workgroups (20 waves at <= 80
-// VGPRs) per CU leave every SIMD 112 VGPRs, one walk wave
-constexpr int kSideBlocksPerCU = 5;
 constexpr int kGroup = 64;             // batches per wave between record walks (one per lane)
 constexpr int kScanBlock = 1024;
 
@@ -46,8 +43,7 @@ constexpr int kMaxRunChunks = 256;
 constexpr uint32_t kRunChunkMin = 16384;
 struct Overlap {
     hipStream_t aux;
-    int chunks;  // chunks per launch_run (1: checksums and walks side by side, no chunks)
-    int grid;    // checksum workgroups when side by side (0: the context's grid)
+    int chunks;  // chunks per launch_run (1: one checksum launch, then its walk)
     hipEvent_t ev[kMaxRunChunks + 1];
 };
 

@@ -455,9 +455,9 @@ __device__ __forceinline__ void process_batch(const uint32_t* __restrict__ sT, c
     STAMP(3);
 }
 
-// One wave per batch, grid-stride; every 64 batches of a wave are walked
-// together.  index_first[i] = local exclusive prefix, block_base[i /
-// kScanBlock] = prefix of earlier scan blocks.
+// One wave per batch, grid-stride: header, both CRCs and the verdict.  The
+// record walk and each batch's index_first are walk_kernel's /
+// walk_wave_kernel's (the plan's local_first / block_base are theirs too).
 __global__ __launch_bounds__(kValidateThreads) void validate_kernel(
     const rpgpu_batch_desc* __restrict__ descs, uint32_t b0, uint32_t n, const uint8_t* __restrict__ data,
     rpgpu_batch_result* __restrict__ res, rpgpu_record_index* __restrict__ index,
@@ -489,8 +489,8 @@ __global__ __launch_bounds__(kValidateThreads) void validate_kernel(
         // one; has_next masks its use): a conditionally initialised struct
         // is lowered to scratch memory
         const rpgpu_batch_desc nd = sload_desc(descs + (has_next ? b + nw : b));
-        // index_first is the walk's to write (walk_kernel / walk_merge_kernel): the
-        // checksums do not wait for the plan
+        // index_first is the walk's to write (walk_kernel): the checksums do not
+        // wait for the plan
         process_batch(sT, d, b, data, res, 0u, pf, nd, has_next DIAG_PASS);
         STAMP(5);
     }
@@ -592,104 +592,6 @@ __global__ __launch_bounds__(256) void walk_wave_kernel(const rpgpu_batch_desc* 
             o[0] = (uint32_t)verdict;
             o[15] = count;
         }
-    }
-}
-
-// The walk side of the concurrent checksum / walk (rpgpu_walk.h): one lane
-// per batch, the header read here (the checks validate_kernel makes before
-// and after the checksums, less the CRCs themselves), the records walked for
-// every batch those checks pass, uncompressed, whose ops ask for a walk --
-// whatever its CRCs turn out to be; walk_merge_kernel decides whether the
-// walk's verdict and entries count.
-__global__ __launch_bounds__(256) void walk_spec_kernel(const rpgpu_batch_desc* __restrict__ descs, uint32_t n,
-                                                        const uint8_t* __restrict__ data,
-                                                        rpgpu_batch_result* __restrict__ res,
-                                                        rpgpu_record_index* __restrict__ index,
-                                                        const uint32_t* __restrict__ local_first,
-                                                        const uint32_t* __restrict__ caps,
-                                                        const uint64_t* __restrict__ block_base, uint64_t index_cap,
-                                                        uint64_t* __restrict__ side) {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    WalkJob J;
-    J.flags = 0;
-    J.body = 0;
-    J.base_offset = J.first_ts = 0;
-    J.n = J.first = J.cap = J.b = 0;
-    J.rc = 0;
-    if (b < n) {
-        const rpgpu_batch_desc d = descs[b];
-        const uint8_t* p = data + d.offset;
-        const uint32_t len = d.length;
-        if ((d.ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX)) && !(d.flags & RPGPU_DESC_NULL_RECORDS) &&
-            len >= (uint32_t)kHeaderSize) {
-            // the header (the arena is readable RPGPU_ARENA_TAIL_PAD bytes past any batch)
-            const u32x4 h0 = ld16(p), h1 = ld16(p + 16), h2 = ld16(p + 32), h3 = ld16(p + 48);
-            Img64 H;
-            H.w[0] = h0.x, H.w[1] = h0.y, H.w[2] = h0.z, H.w[3] = h0.w;
-            H.w[4] = h1.x, H.w[5] = h1.y, H.w[6] = h1.z, H.w[7] = h1.w;
-            H.w[8] = h2.x, H.w[9] = h2.y, H.w[10] = h2.z, H.w[11] = h2.w;
-            H.w[12] = h3.x, H.w[13] = h3.y, H.w[14] = h3.z, H.w[15] = h3.w;
-            bool ok;
-            uint32_t attrs, nb;
-            if (d.format == RPGPU_FMT_KAFKA_WIRE) {
-                // kafka_batch_adapter: magic 2, batch_length + 12 within the data
-                const uint64_t blen = (uint64_t)(int64_t)(int32_t)H.get_be(8, 4) + 12u;
-                ok = H.byte(16) == 2u && blen >= (uint64_t)kHeaderSize && blen <= (uint64_t)len;
-                nb = (uint32_t)blen;
-                attrs = (uint32_t)H.get_be(21, 2);
-                J.base_offset = (int64_t)H.get_be(0, 8);
-                J.first_ts = (int64_t)H.get_be(27, 8);
-                J.rc = (int32_t)H.get_be(57, 4);
-            } else {
-                // parser.cc read_header_impl: not all zero, size_bytes in [61, length]
-                uint32_t any = 0;
-#pragma unroll
-                for (int i = 0; i < 15; i++) any |= H.w[i];
-                any |= H.w[15] & 0xffu;
-                const int32_t sz = (int32_t)H.get_le(4, 4);
-                ok = any != 0 && sz >= kHeaderSize && (uint32_t)sz <= len;
-                nb = (uint32_t)sz;
-                attrs = (uint32_t)H.get_le(21, 2);
-                J.base_offset = (int64_t)H.get_le(8, 8);
-                J.first_ts = (int64_t)H.get_le(27, 8);
-                J.rc = (int32_t)H.get_le(57, 4);
-            }
-            if (ok && (attrs & 7u) == 0) {
-                const uint64_t first = block_base[b / kScanBlock] + local_first[b];
-                uint64_t cap = caps[b];
-                if (first >= index_cap) cap = 0;
-                else if (first + cap > index_cap) cap = index_cap - first;
-                J.body = d.offset + kHeaderSize;
-                J.n = nb - kHeaderSize;
-                J.first = (uint32_t)first;
-                J.cap = (uint32_t)cap;
-                J.b = b;
-                J.flags = kJobLive | ((d.ops & RPGPU_OP_INDEX) ? kJobIndex : 0u);
-            }
-        }
-    }
-    int32_t verdict;
-    uint32_t cnt;
-    walk_batch(data, J, index, verdict, cnt);
-    if (b < n) side[b] = side_word(verdict, cnt);
-}
-
-// After both: the walk's verdict and count for the batches that validated
-// OK, uncompressed, and ask for a walk (walk_kernel's condition).
-__global__ __launch_bounds__(256) void walk_merge_kernel(const rpgpu_batch_desc* __restrict__ descs, uint32_t n,
-                                                         rpgpu_batch_result* __restrict__ res,
-                                                         const uint64_t* __restrict__ side,
-                                                         const uint32_t* __restrict__ local_first,
-                                                         const uint64_t* __restrict__ block_base) {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= n) return;
-    reinterpret_cast<uint32_t*>(res + b)[14] = (uint32_t)(block_base[b / kScanBlock] + local_first[b]);
-    const rpgpu_batch_result& r = res[b];
-    if ((descs[b].ops & (RPGPU_OP_PARSE | RPGPU_OP_INDEX)) && r.verdict == RPGPU_V_OK && r.codec == 0) {
-        const uint64_t w = side[b];
-        uint32_t* o = reinterpret_cast<uint32_t*>(res + b);
-        o[0] = (uint32_t)(int32_t)(uint8_t)(w >> 32);
-        o[15] = (uint32_t)w;
     }
 }
 
@@ -1234,22 +1136,21 @@ hipError_t launch_kafka_codes(const rpgpu_batch_result* d_res, uint32_t n, uint3
 
 // ------------------------------------------------------------ launchers
 // scratch layout: caps[n] u32 | local_first[n] u32 | block_sum[nb] u64 |
-//                 side[n] u64 | wave counters (count, head; 64 B) | wave_list[n] u32
+//                 wave counters (count, head; 64 B) | wave_list[n] u32
 struct WaveWalk {
     uint32_t *list, *count;  // count[0]: batches listed, count[1]: queue head
 };
 static void scratch_parts(void* d_scratch, uint32_t n, uint32_t** caps, uint32_t** local_first,
-                          uint64_t** block_sum, uint64_t** side = nullptr, WaveWalk* ww = nullptr) {
+                          uint64_t** block_sum, WaveWalk* ww = nullptr) {
     uint8_t* sc = static_cast<uint8_t*>(d_scratch);
     *caps = reinterpret_cast<uint32_t*>(sc);
     *local_first = *caps + n;
     const size_t o_bs = ((size_t)n * 8 + 15) & ~(size_t)15;
     *block_sum = reinterpret_cast<uint64_t*>(sc + o_bs);
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
-    const size_t o_side = (o_bs + nb * 8 + 63) & ~(size_t)63;
-    if (side) *side = reinterpret_cast<uint64_t*>(sc + o_side);
+    const size_t o_ww = (o_bs + nb * 8 + 63) & ~(size_t)63;
     if (ww) {
-        ww->count = reinterpret_cast<uint32_t*>(sc + o_side + (size_t)n * 8);
+        ww->count = reinterpret_cast<uint32_t*>(sc + o_ww);
         ww->list = ww->count + 16;
     }
 }
@@ -1274,41 +1175,21 @@ hipError_t launch_block_scan(uint64_t* block_sum, uint32_t nb, uint64_t* total, 
     return hipGetLastError();
 }
 
-// Overlap (RPGPU_OPT_WALK_OVERLAP): either the checksums and the record
-// walks run side by side over the whole arena, one launch each on two
-// streams, finishing each batch through the rpgpu_walk.h handshake
-// (ov->chunks == 1: no grid boundaries), or the arena is checksummed in
-// ov->chunks launches and each chunk's walk runs on the overlap stream while
-// the next chunk is checksummed.  The walk is latency-bound, the checksum
-// bandwidth-bound; they share the CUs (ov->grid: a checksum grid that leaves
-// wave slots for the walk).
+// Overlap (RPGPU_OPT_WALK_OVERLAP): the arena is checksummed in ov->chunks
+// launches and each chunk's walk runs on the overlap stream while the next
+// chunk is checksummed.  The walk is latency-bound, the checksum
+// bandwidth-bound; they share the CUs.  (Checksums and walks side by side in
+// one launch each were measured slower and removed: profiles/r4/NOTES.md r4b.)
 hipError_t launch_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                       rpgpu_batch_result* d_res, rpgpu_record_index* d_index, uint64_t index_cap,
                       const void* d_scratch, const uint32_t* d_tables, int grid, hipStream_t s,
                       const Overlap* ov) {
     if (n == 0) return hipSuccess;
     uint32_t *caps, *local_first;
-    uint64_t *block_sum, *side;
+    uint64_t* block_sum;
     WaveWalk ww;
-    scratch_parts(const_cast<void*>(d_scratch), n, &caps, &local_first, &block_sum, &side, &ww);
+    scratch_parts(const_cast<void*>(d_scratch), n, &caps, &local_first, &block_sum, &ww);
     hipError_t e = hipSuccess;
-    if (ov && n >= kRunChunkMin && ov->chunks == 1) {
-        if ((e = hipEventRecord(ov->ev[0], s)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(ov->aux, ov->ev[0], 0)) != hipSuccess) return e;
-        const uint32_t need = (n + kWavesPerBlock - 1) / kWavesPerBlock;
-        const uint32_t vg = ov->grid > 0 ? (uint32_t)ov->grid : (uint32_t)grid;
-        validate_kernel<<<vg < need ? vg : need, kValidateThreads, 0, s>>>(d_descs, 0, n, d_data, d_res, d_index,
-                                                                            local_first, caps, block_sum, index_cap,
-                                                                            d_tables);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        walk_spec_kernel<<<(n + 255) / 256, 256, 0, ov->aux>>>(d_descs, n, d_data, d_res, d_index, local_first, caps,
-                                                               block_sum, index_cap, side);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        if ((e = hipEventRecord(ov->ev[1], ov->aux)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(s, ov->ev[1], 0)) != hipSuccess) return e;
-        walk_merge_kernel<<<(n + 255) / 256, 256, 0, s>>>(d_descs, n, d_res, side, local_first, block_sum);
-        return hipGetLastError();
-    }
     const uint32_t chunks = (ov && n >= kRunChunkMin) ? (uint32_t)ov->chunks : 1u;
     if ((e = hipMemsetAsync(ww.count, 0, 2 * sizeof(uint32_t), s)) != hipSuccess) return e;
     hipStream_t ws = s;  // the walks' stream
@@ -1378,8 +1259,7 @@ hipError_t validate_occupancy(int* blocks_per_cu) {
 
 size_t validate_scratch_bytes(uint32_t n) {
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
-    return (((((size_t)n * 8 + 15) & ~(size_t)15) + nb * 8 + 63) & ~(size_t)63) + (size_t)n * 8 + 64 +
-           (size_t)n * 4 + 64;
+    return (((((size_t)n * 8 + 15) & ~(size_t)15) + nb * 8 + 63) & ~(size_t)63) + 64 + (size_t)n * 4 + 64;
 }
 
 }  // namespace rpgpu

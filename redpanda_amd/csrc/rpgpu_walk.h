@@ -415,16 +415,5 @@ __device__ __forceinline__ void walk_lanes(const uint8_t* __restrict__ data, Wal
     }
 }
 
-// ---- concurrent checksum and walk (launch_run, Overlap chunks == 1) --------
-// walk_spec_kernel runs beside validate_kernel over the whole arena and stores
-// each batch's walk as one word in side[b] (bits 0..31 index entries written,
-// 32..39 verdict); walk_merge_kernel then gives every batch that validated
-// OK, uncompressed, with a walk asked for, that verdict and count.  No
-// atomics: a returning atomic in the checksum wave would wait for the rows it
-// has in flight (one vmcnt for loads and stores on gfx9).
-__device__ __forceinline__ uint64_t side_word(int32_t verdict, uint32_t count) {
-    return ((uint64_t)(uint8_t)verdict << 32) | count;
-}
-
 }  // namespace rpgpu
 #endif

@@ -78,11 +78,10 @@ def test_crc32c_scalar_mirror(eng):
 def test_walk_overlap_arenas(case, chunks):
     """The walk overlap on an arena above kRunChunkMin (16384 batches):
     chunked checksums with each chunk's walk on a second stream (walk_chunks
-    0 = the default 16, and 7), checksums and speculative walks side by side
-    with a merge (1), and no overlap (-1: RPGPU_OPT_NO_WALK_OVERLAP).  Results
-    and index as the oracle's (uniform small batches, ragged ones whose walks
-    differ in length, corrupted ones -- wire and on-disk -- whose speculative
-    walks must not count), on two launches in a row."""
+    0 = the default 16, and 7), one chunk (1), and no overlap (-1:
+    RPGPU_OPT_NO_WALK_OVERLAP).  Results and index as the oracle's (uniform
+    small batches, ragged ones whose walks differ in length, corrupted ones --
+    wire and on-disk), on two launches in a row."""
     if case in ("corrupt", "disk_corrupt"):
         kw = dict(CASES["headers"], corrupt_ppm=50_000, corrupt_mask=0x1FF)
     else:
