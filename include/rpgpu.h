@@ -195,6 +195,11 @@ typedef struct rpgpu_rp_header {
  * RPGPU_OPT_NO_WALK_OVERLAP checksums the whole arena, then walks it. */
 #define RPGPU_OPT_WALK_OVERLAP 1u
 #define RPGPU_OPT_NO_WALK_OVERLAP 2u
+/* RPGPU_OPT_ZSTD_SPLIT: zstd bodies of lane-sized batches go through the
+ * split decoder (entropy stages with their tables in LDS, then the sequences
+ * executed; rpgpu_zseq.h) instead of the one-lane decoder (tables in HBM).
+ * Same verdicts and bytes; off by default (slower on C4 so far). */
+#define RPGPU_OPT_ZSTD_SPLIT 4u
 
 typedef struct rpgpu_opts {
     uint32_t flags;        /* RPGPU_OPT_* */

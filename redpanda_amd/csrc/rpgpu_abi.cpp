@@ -50,7 +50,7 @@ hipError_t launch_sets_run(const rpgpu_batch_desc* d_sets, uint32_t n, const uin
                            int grid, hipStream_t s, const Overlap* ov);
 hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                               const rpgpu_batch_result* d_vres, uint64_t* d_out_bytes, void* d_scratch,
-                              uint64_t max_decoded, uint32_t ws_cap, hipStream_t s);
+                              uint64_t max_decoded, uint32_t ws_cap, bool zsplit, hipStream_t s);
 hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                              const rpgpu_batch_result* d_vres, rpgpu_decomp_result* d_dres, uint8_t* d_out,
                              uint64_t out_cap, rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_vres2,
@@ -159,6 +159,7 @@ struct rpgpu_ctx {
     bool busy = false;  // one in-flight submission per context (shard-owned)
     uint64_t max_decoded = RPGPU_DEFAULT_MAX_DECODED_BATCH;  // opts.max_decoded_batch
     uint32_t ws_lanes = 0;  // opts.decomp_ws_lanes (0: the default ceiling)
+    bool zsplit = false;    // the split zstd decoder (RPGPU_OPT_ZSTD_SPLIT)
     int efd = -1;       // rpgpu_eventfd: signalled by a host function after each stage
     std::string err;
 };
@@ -237,6 +238,7 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
     // the walk of chunk k beside the checksums of chunk k + 1:
     // on unless RPGPU_OPT_NO_WALK_OVERLAP
     const bool want_overlap = !(opts && (opts->flags & RPGPU_OPT_NO_WALK_OVERLAP));
+    c->zsplit = opts && (opts->flags & RPGPU_OPT_ZSTD_SPLIT);
     if (!want_overlap) c->have_overlap = false;
     std::vector<uint32_t> t(rpgpu::kTableWords);
     rpgpu::build_tables(t.data());
@@ -479,7 +481,7 @@ int32_t rpgpu_decomp_plan_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, 
     if (!c || (n && (!d_descs || !d_data || !d_results || !d_scratch))) return RPGPU_EINVAL;
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     hipError_t e = rpgpu::launch_decomp_plan(d_descs, n, d_data, d_results, d_out_bytes, d_scratch,
-                                              c->max_decoded, c->ws_lanes, s);
+                                              c->max_decoded, c->ws_lanes, c->zsplit, s);
     if (e != hipSuccess) return fail(c, e, "decomp plan launch");
     return RPGPU_OK;
 }

@@ -35,6 +35,7 @@
 #include "rpgpu_device.h"  // before rpgpu_codec.h: HIP attributes
 #include "rpgpu_codec.h"
 #include "rpgpu_zstd.h"
+#include "rpgpu_zseq.h"
 #include "rpgpu_wave.h"
 #include "rpgpu_inflate.h"
 
@@ -123,6 +124,44 @@ size_t zws_offset(uint32_t n) { return counter_offset(n) + 256 + (size_t)decomp_
 size_t parts_offset(uint32_t n, uint32_t cap) {
     return (zws_offset(n) + ws_region(n, cap) + 255) & ~(size_t)255;
 }
+// the split zstd decoder's per-list-entry state (rpgpu_zseq.h), after the parts:
+// flag[n] u32 (bit 0 planned, 1 handed back, 2 execute) | lits[n] u64 | recs[n] u64
+// (local prefixes) | lit / rec block sums [nb] u64 each | section words [n][kMaxSec] u32
+size_t zseq_offset(uint32_t n, uint32_t cap) {
+    return (parts_offset(n, cap) + (size_t)part_cap(n) * (sizeof(SplitPart) + sizeof(int32_t)) + 255) & ~(size_t)255;
+}
+#ifdef RPZS_HBM_WS  // diagnostics build: A1 / A2 workspaces in HBM, one per zstd lane
+constexpr size_t kZsWs = sizeof(rpzstd::SeqWs) > sizeof(rpzstd::HufWs) ? sizeof(rpzstd::SeqWs) : sizeof(rpzstd::HufWs);
+#else
+constexpr size_t kZsWs = 0;
+#endif
+size_t zseq_bytes(uint32_t n) {
+    const size_t nb = (n + kScanBlock - 1) / kScanBlock;
+    return (size_t)n * (4 + 8 + 8 + 4 + 4 + 4 * rpzstd::kMaxSec) + 2 * nb * 8 + 64 +
+           (size_t)(n < RPZ_LANES ? n : RPZ_LANES) * ((kZsWs + 15) & ~(size_t)15);
+}
+struct ZParts {
+    uint8_t* hws;  // RPZS_HBM_WS: the lanes' workspaces
+    uint32_t* flag;
+    uint64_t *lits, *recs, *bs_l, *bs_r;  // exclusive prefixes within scan blocks, block prefixes
+    uint32_t *szl, *szr;                   // the plan's literal bytes / records per entry
+    uint32_t* sec;
+};
+ZParts zparts(void* p, uint32_t n, uint32_t cap) {
+    const size_t nb = (n + kScanBlock - 1) / kScanBlock;
+    uint8_t* b = static_cast<uint8_t*>(p) + zseq_offset(n, cap);
+    ZParts z;
+    z.lits = reinterpret_cast<uint64_t*>(b);
+    z.recs = z.lits + n;
+    z.bs_l = z.recs + n;
+    z.bs_r = z.bs_l + nb;
+    z.flag = reinterpret_cast<uint32_t*>(z.bs_r + nb);
+    z.szl = z.flag + n;
+    z.szr = z.szl + n;
+    z.sec = z.szr + n;
+    z.hws = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(z.sec + (size_t)n * rpzstd::kMaxSec) + 63) & ~(uintptr_t)63);
+    return z;
+}
 Parts parts(void* p, uint32_t n, uint32_t cap) {
     uint8_t* b = static_cast<uint8_t*>(p);
     Parts s;
@@ -142,9 +181,7 @@ Parts parts(void* p, uint32_t n, uint32_t cap) {
 }
 }  // namespace
 
-size_t decomp_scratch_bytes(uint32_t n, uint32_t ws_cap) {
-    return parts_offset(n, ws_cap) + (size_t)part_cap(n) * (sizeof(SplitPart) + sizeof(int32_t));
-}
+size_t decomp_scratch_bytes(uint32_t n, uint32_t ws_cap) { return zseq_offset(n, ws_cap) + zseq_bytes(n); }
 
 // slots above this go to the wave decoders (a lane's serial decode of a
 // large body would hold up the whole launch)
@@ -169,6 +206,12 @@ static_assert(kSplitMinSlot <= kLaneMaxSlot, "split threshold above the lane dec
 // bound -- no output reserved (the scan counts 0), verdict DECOMP_OVERFLOW
 // with out_len = the bound, the capacity a retry needs (rpgpu_decompress_batch)
 constexpr uint64_t kOverCeiling = 1ull << 63;
+
+// the split zstd decoder's per-entry flags (zseq_*_kernel below)
+constexpr uint32_t kZPlanned = 1, kZBack = 2, kZExec = 4, kZOver = 8;
+__device__ __forceinline__ uint64_t cnt64(const uint32_t* c, int k) {
+    return (uint64_t)c[k] | ((uint64_t)c[k + 1] << 32);
+}
 
 __device__ __forceinline__ bool decomp_wanted(const rpgpu_batch_desc& d, const rpgpu_batch_result& v) {
     return (d.ops & RPGPU_OP_DECOMP) && v.verdict == RPGPU_V_OK && v.codec != 0;
@@ -295,8 +338,9 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
                 sc = np;
             } else {
                 // the reservation ran past the part list: the slots it holds
-                // below the end carry no part (part_kernel skips them), the
-                // batch goes to the wave decoder
+                // below the end carry no part (part_kernel skips them); the
+                // batch is decoded unsplit -- by the lane decoder when its slot
+                // is at most kLaneMaxSlot, else by the wave decoder
                 for (uint32_t k = k0; k < half && k < k0 + np; k++) {
                     SplitPart t;
                     t.batch = i, t.kind = kSkipPart, t.in_off = t.in_len = 0;
@@ -474,7 +518,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_WS_WA
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
     rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
     rpgpu_batch_desc* __restrict__ out_descs, void* __restrict__ wsraw, uint32_t* __restrict__ counter,
-    uint32_t* __restrict__ zlist) {
+    uint32_t* __restrict__ zlist, const uint32_t* __restrict__ zflag) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     // gzip: every batch index, 2 KB workspaces in the scratch; zstd: the plan's
     // list, `zl` workspaces after the output slots (decomp_ws_kernel)
@@ -483,7 +527,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_WS_WA
     uint8_t* zbase = nullptr;
     if (FAM == 4) {
         cnt = counter[7];
-        lanes = counter[10];
+        // the plan's lane count, clamped to this grid (a plan made with a larger
+        // cap must not leave list entries past the grid undecoded)
+        lanes = counter[10] < lanes ? counter[10] : lanes;
         const uint64_t ws_off = (uint64_t)counter[8] | ((uint64_t)counter[9] << 32);
         ws_end = ws_off + (uint64_t)lanes * sizeof(rpzstd::Ws);
         zbase = out + ws_off;
@@ -491,6 +537,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_WS_WA
     if (g >= n || g >= lanes) return;  // lanes past the arena / the list own no workspace
     rpinfl::Ws& gws = reinterpret_cast<rpinfl::Ws*>(wsraw)[g];
     for (uint32_t k = g; k < cnt; k += lanes) {
+        // zstd: the split decoder's batches unless it handed them back
+        if (FAM == 4 && (zflag[k] & (kZPlanned | kZBack)) == kZPlanned) continue;
         const uint32_t i = FAM == 4 ? zlist[k] : k;
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
@@ -534,7 +582,9 @@ __global__ __launch_bounds__(256) void zstd_ring_kernel(
     rpgpu_batch_desc* __restrict__ out_descs, const uint32_t* __restrict__ counter,
     const uint32_t* __restrict__ zlist) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t cnt = counter[11], lanes = counter[10] < cnt ? counter[10] : cnt;
+    uint32_t lanes = counter[10] < gridDim.x * blockDim.x ? counter[10] : gridDim.x * blockDim.x;
+    const uint32_t cnt = counter[11];
+    if (cnt < lanes) lanes = cnt;
     if (g >= lanes) return;
     const uint32_t* rlist = zlist + counter[7];
     const uint64_t ws_off = (uint64_t)counter[8] | ((uint64_t)counter[9] << 32);
@@ -554,6 +604,186 @@ __global__ __launch_bounds__(256) void zstd_ring_kernel(
     }
 }
 
+
+// ---------------------------------------------------- split zstd decoder
+// (rpgpu_zseq.h).  Counters: [16..17] literal bytes planned, [18..19] records
+// planned (u64 totals of the scans), [20..21] / [22..23] the literal / record
+// regions' offsets in the output buffer (after the lane workspaces).
+// zflag per zstd lane list entry: bit 0 planned for the split path, 1 handed
+// back to the one-lane decoder, 2 execute (verdict OK), 3 A1 ran out of room.
+
+// per zstd lane list entry: eligibility and reservations, scanned per workgroup
+__global__ __launch_bounds__(kScanBlock) void zseq_plan_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data,
+    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot, const uint32_t* __restrict__ counter,
+    const uint32_t* __restrict__ zlist, uint32_t* __restrict__ flag, uint64_t* __restrict__ lits,
+    uint64_t* __restrict__ recs, uint64_t* __restrict__ bs_l, uint64_t* __restrict__ bs_r, uint32_t* __restrict__ szl,
+    uint32_t* __restrict__ szr, uint32_t n, bool enabled) {
+    __shared__ uint64_t wl[kScanBlock / 64], wr[kScanBlock / 64];
+    const uint32_t k = blockIdx.x * kScanBlock + threadIdx.x;
+    const uint32_t cnt = counter[7];
+    uint64_t a = 0, r = 0;
+    if (k < cnt) {
+        const uint32_t i = zlist[k];
+        const rpgpu_batch_desc d = descs[i];
+        const rpgpu_batch_result v = vres[i];
+        const uint64_t sz = slot[i];
+        uint32_t f = 0;
+        if (enabled && decomp_wanted(d, v) && v.codec == 4 && !(sz & kOverCeiling) && sz != 0 && sz <= lane_max(4)) {
+            const rpzstd::Plan pl = rpzstd::plan(data + d.offset + kHeaderSize, body_len(v));
+            if (pl.ok && pl.lits < (1ull << 31) && pl.recs < (1ull << 31)) {
+                f = kZPlanned;
+                a = pl.lits;
+                r = pl.recs;
+            }
+        }
+        flag[k] = f;
+        szl[k] = (uint32_t)a;
+        szr[k] = (uint32_t)r;
+    }
+    const uint32_t l = lane_id();
+    uint64_t x = a, y = r;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+        const uint32_t lo = __shfl_up((uint32_t)x, s, 64), hi = __shfl_up((uint32_t)(x >> 32), s, 64);
+        const uint32_t plo = __shfl_up((uint32_t)y, s, 64), phi = __shfl_up((uint32_t)(y >> 32), s, 64);
+        if (l >= (uint32_t)s) {
+            x += ((uint64_t)hi << 32) | lo;
+            y += ((uint64_t)phi << 32) | plo;
+        }
+    }
+    const uint32_t wv = threadIdx.x >> 6;
+    if (l == 63) {
+        wl[wv] = x;
+        wr[wv] = y;
+    }
+    __syncthreads();
+    uint64_t bl = 0, br = 0;
+    for (uint32_t q = 0; q < wv; q++) {
+        bl += wl[q];
+        br += wr[q];
+    }
+    if (k < n) {
+        lits[k] = bl + x - a;
+        recs[k] = br + y - r;
+    }
+    if (threadIdx.x == kScanBlock - 1) {
+        bs_l[blockIdx.x] = bl + x;
+        bs_r[blockIdx.x] = br + y;
+    }
+}
+
+// A1: literal sections (Huffman tables in LDS, one HufWs per lane)
+#ifdef RPZS_HBM_WS
+#define RPZS_WG 256
+#else
+#define RPZS_WG 64
+#endif
+__global__ __launch_bounds__(RPZS_WG) void zseq_lit_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data,
+    const rpgpu_batch_result* __restrict__ vres, const uint32_t* __restrict__ counter,
+    const uint32_t* __restrict__ zlist, uint32_t* __restrict__ flag, const uint64_t* __restrict__ lits,
+    const uint64_t* __restrict__ bs_l, const uint32_t* __restrict__ szl, uint32_t* __restrict__ sec_all,
+    uint8_t* __restrict__ out, uint32_t per_wg, uint8_t* __restrict__ hws) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+    const uint32_t l = threadIdx.x;
+    if (l >= per_wg) return;
+#ifdef RPZS_HBM_WS
+    rpzstd::HufWs& w = *reinterpret_cast<rpzstd::HufWs*>(hws + (size_t)(blockIdx.x * per_wg + l) * ((kZsWs + 15) & ~(size_t)15));
+#else
+    rpzstd::HufWs& w = reinterpret_cast<rpzstd::HufWs*>(dyn_lds)[l];
+#endif
+    const uint32_t cnt = counter[7], lanes = gridDim.x * per_wg;
+    const uint64_t loff = cnt64(counter, 20);
+    for (uint32_t k = blockIdx.x * per_wg + l; k < cnt; k += lanes) {
+        if (!(flag[k] & kZPlanned)) continue;
+        const uint32_t i = zlist[k];
+        const rpgpu_batch_desc d = descs[i];
+        const rpgpu_batch_result v = vres[i];
+        uint32_t* sec = sec_all + (size_t)k * rpzstd::kMaxSec;
+        for (uint32_t j = 0; j < rpzstd::kMaxSec; j++) sec[j] = 0;
+        rpzstd::LitEmit em{out + loff + bs_l[k / kScanBlock] + lits[k], szl[k], 0, sec, -1, false};
+        rpzstd::lit_walk(em, w, data + d.offset + kHeaderSize, body_len(v));
+        flag[k] = kZPlanned | (em.over ? kZOver : 0u);
+    }
+}
+
+// A2: the restatement's decisions, copies written as records (SeqWs in LDS).
+// Decides the batch's verdict and decoded length, or hands it back.
+__global__ __launch_bounds__(RPZS_WG) void zseq_seq_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data,
+    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
+    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
+    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
+    rpgpu_batch_desc* __restrict__ out_descs, const uint32_t* __restrict__ counter,
+    const uint32_t* __restrict__ zlist, uint32_t* __restrict__ flag, const uint64_t* __restrict__ lits,
+    const uint64_t* __restrict__ bs_l, const uint32_t* __restrict__ szl, const uint64_t* __restrict__ recs,
+    const uint64_t* __restrict__ bs_r, const uint32_t* __restrict__ szr, const uint32_t* __restrict__ sec_all,
+    uint32_t per_wg, uint8_t* __restrict__ hws) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+    const uint32_t l = threadIdx.x;
+    if (l >= per_wg) return;
+#ifdef RPZS_HBM_WS
+    rpzstd::SeqWs& w = *reinterpret_cast<rpzstd::SeqWs*>(hws + (size_t)(blockIdx.x * per_wg + l) * ((kZsWs + 15) & ~(size_t)15));
+#else
+    rpzstd::SeqWs& w = reinterpret_cast<rpzstd::SeqWs*>(dyn_lds)[l];
+#endif
+    const uint32_t cnt = counter[7], lanes = gridDim.x * per_wg;
+    const uint64_t loff = cnt64(counter, 20), roff = cnt64(counter, 22);
+    // the regions must lie inside the caller's buffer, else the one-lane decoder decides
+    const bool fits = roff + (cnt64(counter, 18) + 16) * 8 <= out_cap;
+    for (uint32_t k = blockIdx.x * per_wg + l; k < cnt; k += lanes) {
+        const uint32_t f = flag[k];
+        if (!(f & kZPlanned)) continue;
+        if (!fits) {
+            flag[k] = kZPlanned | kZBack;
+            continue;
+        }
+        const uint32_t i = zlist[k];
+        const rpgpu_batch_desc d = descs[i];
+        const rpgpu_batch_result v = vres[i];
+        uint64_t sz = slot[i];
+        const uint64_t off = block_base[i / kScanBlock] + local[i];
+        int32_t verdict = RPGPU_V_SKIPPED;
+        uint64_t len = 0;
+        uint32_t nf = kZPlanned;
+        if (plan_slot(sz, off, out_cap, verdict, len)) {
+            rpzstd::SeqEmit em{sec_all + (size_t)k * rpzstd::kMaxSec, -1, out + loff + bs_l[k / kScanBlock] + lits[k],
+                               szl[k], 0, reinterpret_cast<uint64_t*>(out + roff) + bs_r[k / kScanBlock] + recs[k],
+                               0, szr[k], nullptr, 0, (f & kZOver) != 0};
+            verdict = rpzstd::uncompress<false>(em, data + d.offset + kHeaderSize, body_len(v), out + off + kHeaderSize,
+                                                sz - kHeaderSize - rpcodec::kSlack, &len, w);
+            em.put(rpzstd::rec_op(rpzstd::kOpEnd, 0));
+            if (em.fb || verdict == rpzstd::V_RING) {
+                flag[k] = kZPlanned | kZBack;
+                continue;
+            }
+            if (verdict == RPGPU_V_OK) nf |= kZExec;
+        }
+        finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
+        flag[k] = nf;
+    }
+}
+
+// B: the records of every batch A2 decided OK, one lane per batch
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_WAVES))) void zseq_exec_kernel(
+    const uint32_t* __restrict__ counter, const uint32_t* __restrict__ zlist, const uint32_t* __restrict__ flag,
+    const uint64_t* __restrict__ recs, const uint64_t* __restrict__ bs_r, const uint64_t* __restrict__ local,
+    const uint64_t* __restrict__ block_base, uint8_t* __restrict__ out) {
+    const uint32_t cnt = counter[7], lanes = gridDim.x * blockDim.x;
+    const uint64_t roff = cnt64(counter, 22);
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += lanes) {
+        if ((flag[k] & (kZExec | kZBack)) != kZExec) continue;
+#ifdef RPZS_DIAG_NORECS
+        continue;
+#endif
+        const uint32_t i = zlist[k];
+        const uint64_t off = block_base[i / kScanBlock] + local[i];
+        rpzstd::exec_lane(reinterpret_cast<const uint64_t*>(out + roff) + bs_r[k / kScanBlock] + recs[k],
+                          out + off + kHeaderSize);
+    }
+}
+
 // After the plan's scan: the zstd lane workspaces go after the output slots
 // (256-byte aligned), min(listed zstd lane batches, cap) of them; the plan's
 // output bytes include them.  counter[8..9] = their offset, [10] = lanes.
@@ -565,7 +795,15 @@ __global__ void decomp_ws_kernel(uint32_t* __restrict__ counter, uint32_t cap, u
     counter[8] = (uint32_t)off;
     counter[9] = (uint32_t)(off >> 32);
     counter[10] = lanes;
-    if (out_bytes) *out_bytes = lanes ? off + (uint64_t)lanes * sizeof(rpzstd::Ws) : slots;
+    // the split decoder's literal and record regions (64 bytes / 16 records of padding)
+    const uint64_t ws_end = lanes ? off + (uint64_t)lanes * sizeof(rpzstd::Ws) : slots;
+    const uint64_t loff = (ws_end + 255) & ~(uint64_t)255;
+    const uint64_t roff = (loff + cnt64(counter, 16) + 64 + 255) & ~(uint64_t)255;
+    counter[20] = (uint32_t)loff;
+    counter[21] = (uint32_t)(loff >> 32);
+    counter[22] = (uint32_t)roff;
+    counter[23] = (uint32_t)(roff >> 32);
+    if (out_bytes) *out_bytes = lanes ? roff + (cnt64(counter, 18) + 16) * 8 : slots;
 }
 
 // One batch body through the codec restatement, bytes produced by the wave.
@@ -749,9 +987,45 @@ __global__ void decomp_counters_kernel(uint32_t* c, uint32_t run) {
 }
 
 // ------------------------------------------------------------ launchers
+// the split zstd decoder's LDS geometry: RPZS_WAVES one-wave workgroups per CU
+// share the CU's LDS, each with as many lanes as their workspaces fit in its
+// share (RPZS_LDS_BYTES overrides the CU's LDS size).  The lanes decode serial
+// chains at LDS latency: spread over waves (two per SIMD) they hide each
+// other's latency, where one wave of 56 lanes per CU would not.
+struct ZLaunch {
+    uint32_t grid, lit_lanes, seq_lanes;
+};
+#ifndef RPZS_LDS_BYTES
+#define RPZS_LDS_BYTES 0
+#endif
+#ifndef RPZS_WAVES
+#define RPZS_WAVES 8
+#endif
+ZLaunch zseq_launch() {
+    static ZLaunch z{0, 0, 0};
+    if (z.grid) return z;
+    int dev = 0, cus = 0, lds = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
+    if (RPZS_LDS_BYTES) lds = RPZS_LDS_BYTES;
+    if (lds < (int)sizeof(rpzstd::SeqWs)) lds = (int)sizeof(rpzstd::SeqWs);
+    auto fit = [&](size_t each) {
+        const size_t k = (size_t)lds / RPZS_WAVES / each;
+        return (uint32_t)(k > 64 ? 64 : k < 1 ? 1 : k);
+    };
+    ZLaunch t{(uint32_t)((cus > 0 ? cus : 256) * RPZS_WAVES), fit(sizeof(rpzstd::HufWs)), fit(sizeof(rpzstd::SeqWs))};
+    hipFuncSetAttribute(reinterpret_cast<const void*>(zseq_lit_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)(t.lit_lanes * sizeof(rpzstd::HufWs)));
+    hipFuncSetAttribute(reinterpret_cast<const void*>(zseq_seq_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)(t.seq_lanes * sizeof(rpzstd::SeqWs)));
+    z = t;
+    return z;
+}
+
 hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                               const rpgpu_batch_result* d_vres, uint64_t* d_out_bytes, void* d_scratch,
-                              uint64_t max_decoded, uint32_t ws_cap, hipStream_t s) {
+                              uint64_t max_decoded, uint32_t ws_cap, bool zsplit, hipStream_t s) {
     if (n == 0) return d_out_bytes ? hipMemsetAsync(d_out_bytes, 0, sizeof(uint64_t), s) : hipSuccess;
     const Parts p = parts(d_scratch, n, ws_cap);
     const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
@@ -770,6 +1044,13 @@ hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const
     if (e != hipSuccess) return e;
     decomp_counters_kernel<<<1, 64, 0, s>>>(p.counter, 0);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    // the split zstd decoder's reservations over the zstd lane list
+    const ZParts z = zparts(d_scratch, n, ws_cap);
+    zseq_plan_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, d_data, d_vres, p.slot, p.counter, p.wlist + 2 * (size_t)n,
+                                               z.flag, z.lits, z.recs, z.bs_l, z.bs_r, z.szl, z.szr, n, zsplit);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = launch_block_scan(z.bs_l, nb, reinterpret_cast<uint64_t*>(p.counter + 16), s)) != hipSuccess) return e;
+    if ((e = launch_block_scan(z.bs_r, nb, reinterpret_cast<uint64_t*>(p.counter + 18), s)) != hipSuccess) return e;
     if ((e = launch_block_scan(p.block_sum, nb, reinterpret_cast<uint64_t*>(p.counter + 8), s)) != hipSuccess) return e;
     decomp_ws_kernel<<<1, 64, 0, s>>>(p.counter, zstd_lanes(n, ws_cap), d_out_bytes);
     return hipGetLastError();
@@ -829,9 +1110,33 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                                               out_cap, d_out_descs, p.scount);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t zl = zstd_lanes(n, ws_cap);  // the HBM-workspace lane decoder (at most zl lanes)
+    // the split decoder over the zstd lane batches it planned: A1 literals, A2
+    // decisions + records, B execution; what A2 hands back, the one-lane decoder
+    const ZParts z = zparts(d_scratch, n, ws_cap);
+    {
+#ifdef RPZS_HBM_WS
+        const uint32_t zl_n = n < RPZ_LANES ? n : RPZ_LANES;
+        const ZLaunch zq{(zl_n + 255) / 256, 256, 256};
+        const size_t lit_lds = 0, seq_lds = 0;
+#else
+        const ZLaunch zq = zseq_launch();
+        const size_t lit_lds = zq.lit_lanes * sizeof(rpzstd::HufWs), seq_lds = zq.seq_lanes * sizeof(rpzstd::SeqWs);
+#endif
+        zseq_lit_kernel<<<zq.grid, RPZS_WG, lit_lds, s>>>(
+            d_descs, d_data, d_vres, p.counter, p.wlist + 2 * (size_t)n, z.flag, z.lits, z.bs_l, z.szl, z.sec, d_out,
+            zq.lit_lanes, z.hws);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        zseq_seq_kernel<<<zq.grid, RPZS_WG, seq_lds, s>>>(
+            d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.counter,
+            p.wlist + 2 * (size_t)n, z.flag, z.lits, z.bs_l, z.szl, z.recs, z.bs_r, z.szr, z.sec, zq.seq_lanes, z.hws);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        zseq_exec_kernel<<<(zl + 255) / 256, 256, 0, s>>>(p.counter, p.wlist + 2 * (size_t)n, z.flag, z.recs, z.bs_r,
+                                                         p.local, p.block_sum, d_out);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     ws_lane_kernel<4><<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres,
                                                          d_out, out_cap, d_out_descs, nullptr, p.counter,
-                                                         p.wlist + 2 * (size_t)n);
+                                                         p.wlist + 2 * (size_t)n, z.flag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     zstd_ring_kernel<<<(zl + 255) / 256, 256, 0, s>>>(d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres,
                                                       d_out, out_cap, d_out_descs, p.counter, p.wlist + 2 * (size_t)n);
@@ -839,7 +1144,7 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     const uint32_t gl = gzip_lanes(n, ws_cap);
     ws_lane_kernel<1><<<(gl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
                                                          d_dres, d_out, out_cap, d_out_descs, p.gws, p.counter,
-                                                         nullptr);
+                                                         nullptr, nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ds) {
         if ((e = hipEventRecord(ds->join, ds->aux)) != hipSuccess) return e;

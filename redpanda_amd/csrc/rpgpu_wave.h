@@ -179,6 +179,14 @@ struct WaveEmit {
     const uint8_t* lsrc;
     uint64_t ll, ml, off;
 
+    __device__ __forceinline__ void section_begin() {}
+    __device__ __forceinline__ int64_t table(rpzstd::Ws& w, const uint8_t* src, uint64_t n) {
+        return rpzstd::huf_read_table(w, src, n);
+    }
+    __device__ __forceinline__ bool checksum(const uint8_t* p, uint64_t n, uint32_t want) {
+        sync();  // the checksum reads the decoded bytes
+        return (uint32_t)rpzstd::xxh64(p, n) == want;
+    }
     __device__ __forceinline__ void init(uint8_t* scr) {
         gbase = gend = nullptr;
         plsrc = nullptr;

@@ -249,7 +249,9 @@ struct ByteOut {
 RPC_HD void bo_put(ByteOut& o, uint32_t v) {
     o.acc |= (uint64_t)(v & 0xFF) << (8 * o.n);
     if (++o.n == 8) {
+#ifndef RPZS_DIAG_NOLITST  // diagnostics build: decoded literals not stored (timing only)
         __builtin_memcpy(o.p, &o.acc, 8);
+#endif
         o.p += 8;
         o.acc = 0;
         o.n = 0;
@@ -275,6 +277,7 @@ RPC_HD bool huf_select_x2(uint64_t dst, uint64_t csrc) {
 // without the X1 table, for one workspace per lane in LDS, measured 5.5x
 // slower per C4 step in round 3 and was removed.)
 struct Ws {
+    static constexpr bool kHasX = true;  // llx / mlx (filled for workspaces in LDS)
     uint16_t huf[1u << kHufMaxLog];  // X1 table: symbol | nbBits << 8
     uint16_t huf1[1u << kHuf1Log];   // huf by the first kHuf1Log bits where that decides the code, else kHuf1None
     uint32_t ll[512], ml[512], of[256];  // sequence tables: state << 16 | nbBits << 8 | symbol
@@ -494,9 +497,13 @@ RPC_HD int64_t read_ncount(int16_t* norm, uint32_t* max_sv, uint32_t* table_log,
 }
 
 // FSE decoding table (FSE_buildDTable / ZSTD_buildFSETable): cell =
-// newState << 16 | nbBits << 8 | symbol.  Returns fastMode (no symbol at or
-// above half the table).
-RPC_HD bool build_fse(uint32_t* t, uint16_t* next, const int16_t* norm, uint32_t max_sv, uint32_t log) {
+// newState << 16 | nbBits << 8 | symbol; in the 16-bit form (T = uint16_t,
+// the split decoder's LDS tables, rpgpu_zseq.h) cell = nextState << 6 |
+// symbol, from which nbBits = log - highbit(nextState) and newState =
+// (nextState << nbBits) - size follow (fse_cell16).  Returns fastMode (no
+// symbol at or above half the table).
+template <class T>
+RPC_HD bool build_fse(T* t, uint16_t* next, const int16_t* norm, uint32_t max_sv, uint32_t log) {
     const uint32_t size = 1u << log, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
     uint32_t high = size - 1;
     const int16_t large = (int16_t)(1 << (log - 1));
@@ -521,10 +528,21 @@ RPC_HD bool build_fse(uint32_t* t, uint16_t* next, const int16_t* norm, uint32_t
     for (uint32_t u = 0; u < size; u++) {
         const uint32_t s = t[u] & 0xFF;
         const uint32_t ns = next[s]++;
-        const uint32_t nb = log - hb32(ns);
-        t[u] = (((ns << nb) - size) << 16) | (nb << 8) | s;
+        if constexpr (sizeof(T) == 2) {
+            t[u] = (T)((ns << 6) | s);
+        } else {
+            const uint32_t nb = log - hb32(ns);
+            t[u] = (((ns << nb) - size) << 16) | (nb << 8) | s;
+        }
     }
     return fast;
+}
+
+// a decoding cell in build_fse's 32-bit layout, from either form
+RPC_HD uint32_t fse_cell(const uint32_t* t, uint32_t, uint32_t s) { return t[s]; }
+RPC_HD uint32_t fse_cell(const uint16_t* t, uint32_t log, uint32_t s) {
+    const uint32_t c = t[s], ns = c >> 6, nb = log - hb32(ns);
+    return (((ns << nb) - (1u << log)) << 16) | (nb << 8) | (c & 63u);
 }
 
 // ---------------------------------------------------------------- Huffman
@@ -591,8 +609,14 @@ RPC_HD int64_t huf_read_table(W& w, const uint8_t* in, uint64_t n) {
         w.rank[last]++;
     }
     if (w.rank[1] < 2 || (w.rank[1] & 1)) return RPZ_FAIL(-1);
-    const uint32_t nsym = (uint32_t)oSize + 1;
-    // X1 table: ranks by weight ascending, symbols in order within a weight
+    huf_fill(w, (uint32_t)oSize + 1, log);
+    return (int64_t)iSize + 1;
+}
+
+// The X1 table (HUF_readDTableX1) of weights w.w[0, nsym) with w.rank = the
+// count per weight: ranks by weight ascending, symbols in order within a
+// weight.  Workspaces in HBM also get the first-level table huf1.
+RPC_HD void huf_fill(Ws& w, uint32_t nsym, uint32_t log) {
     {
         uint32_t start = 0;
         for (uint32_t r = 1; r <= log; r++) {
@@ -616,7 +640,6 @@ RPC_HD int64_t huf_read_table(W& w, const uint8_t* in, uint64_t n) {
                 w.huf1[i] = (e >> 8) <= kHuf1Log ? e : kHuf1None;
             }
     }
-    return (int64_t)iSize + 1;
 }
 
 // One Huffman stream: `nsym` symbols, the first `nwrite` stored to out.
@@ -731,8 +754,17 @@ struct Huf4 {
 // interleaved one symbol each per step.  The device's wave-cooperative
 // emitter (rpgpu_wave.h) decodes the four streams on four lanes into a
 // scratch buffer and executes sequences 64 at a time with the whole wave.
+RPC_HD uint64_t xxh64(const uint8_t* p, uint64_t len);
 struct DirectEmit {
     static constexpr bool kInlineBlocks = false;
+    // hooks of the split decoder (rpgpu_zseq.h): a literals section begins, its
+    // Huffman table is read, a frame checksum is checked over the decoded bytes
+    RPC_HD void section_begin() {}
+    template <class W>
+    RPC_HD int64_t table(W& w, const uint8_t* src, uint64_t n) {
+        return huf_read_table(w, src, n);
+    }
+    RPC_HD bool checksum(const uint8_t* p, uint64_t n, uint32_t want) { return (uint32_t)xxh64(p, n) == want; }
 #ifdef RPGPU_DIAG_NOCOPY  // diagnostics build only: the decode without its sequence copies
     RPC_HD void lits(uint8_t*, const uint8_t*, uint64_t) {}
     RPC_HD void match(uint8_t*, uint64_t, uint64_t) {}
@@ -749,6 +781,12 @@ struct DirectEmit {
     RPC_HD bool huf1(const W& w, const uint8_t* src, uint64_t len, uint8_t* d, uint64_t n) {
         return huf_stream(w, src, len, d, n, n, w.huf1_on != 0);  // Ws in HBM: the first-level table
     }
+#ifdef RPGPU_DIAG_ZSTD_NOHUF  // diagnostics build only: the Huffman literal streams not decoded
+    template <class W>
+    RPC_HD bool huf4(const W&, const Huf4&) {
+        return true;
+    }
+#else
     template <class W>
     RPC_HD bool huf4(const W& w, const Huf4& a) {
         const uint32_t L = w.huf_log;
@@ -771,6 +809,7 @@ struct DirectEmit {
         }
         return h0.ok && h1.ok && h2.ok && h3.ok;
     }
+#endif
 };
 
 // ---------------------------------------------------------------- blocks
@@ -784,6 +823,7 @@ struct Lit {
 template <class E, class W>
 RPZ_COLD int64_t literals(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t op, uint64_t tail,
                           Lit& lit) {
+    em.section_begin();  // one literals section per compressed block (rpgpu_zseq.h numbers them)
     if (n < 3) return RPZ_FAIL(-1);  // MIN_CBLOCK_SIZE
     const uint32_t type = in[0] & 3, lh = (in[0] >> 2) & 3;
     if (type == 0 || type == 1) {  // raw / RLE
@@ -845,7 +885,7 @@ RPZ_COLD int64_t literals(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* o
         } else {
             w.huf_x2 = 0;  // HUF_decompress1X1_DCtx_wksp
         }
-        const int64_t th = huf_read_table(w, src, slen);
+        const int64_t th = em.table(w, src, slen);
         if (th < 0 || (uint64_t)th >= slen) return RPZ_FAIL(-1);
         src += th;
         slen -= (uint64_t)th;
@@ -894,8 +934,8 @@ RPZ_COLD int64_t literals(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* o
     return (int64_t)(hs + csize);
 }
 
-RPC_HD void build_default(uint32_t* t, uint16_t* next, int16_t* norm, const int8_t* dn, uint32_t max_sv,
-                          uint32_t log) {
+template <class T>
+RPC_HD void build_default(T* t, uint16_t* next, int16_t* norm, const int8_t* dn, uint32_t max_sv, uint32_t log) {
     for (uint32_t s = 0; s <= max_sv; s++) norm[s] = dn[s];
     build_fse(t, next, norm, max_sv, log);
 }
@@ -918,15 +958,17 @@ RPC_HD int64_t seq_table_impl(W& w, uint32_t mode, uint32_t which, const uint8_t
 // in LDS, where they save a dependent lookup; a workspace in HBM reads the
 // baselines from the 89-entry code tables instead (one cached line, not a
 // line of HBM per sequence)
-template <class W>
-RPC_HD int64_t seq_table(W& w, uint32_t mode, uint32_t which, const uint8_t* in, uint64_t n, bool extra) {
+template <bool kExtra, class W>
+RPC_HD int64_t seq_table(W& w, uint32_t mode, uint32_t which, const uint8_t* in, uint64_t n) {
     const int64_t h = seq_table_impl(w, mode, which, in, n);
-    if (extra && h >= 0 && mode != 3) seq_extra(w, which);
+    if constexpr (kExtra) {
+        if (h >= 0 && mode != 3) seq_extra(w, which);
+    }
     return h;
 }
 template <class W>
 RPC_HD int64_t seq_table_impl(W& w, uint32_t mode, uint32_t which, const uint8_t* in, uint64_t n) {
-    uint32_t* t = which == 0 ? w.ll : (which == 1 ? w.of : w.ml);
+    auto* t = which == 0 ? w.ll : (which == 1 ? w.of : w.ml);
     uint8_t& log = which == 0 ? w.ll_log : (which == 1 ? w.of_log : w.ml_log);
     const uint32_t max = which == 0 ? 35u : (which == 1 ? 31u : 52u);
     const uint32_t max_log = which == 1 ? 8u : 9u;
@@ -934,7 +976,8 @@ RPC_HD int64_t seq_table_impl(W& w, uint32_t mode, uint32_t which, const uint8_t
     case 1:  // RLE
         if (n == 0) return RPZ_FAIL(-1);
         if (in[0] > max) return RPZ_FAIL(-1);
-        t[0] = in[0];
+        // the one state reads no bits and keeps its baseline 0 (16-bit form: nextState 1)
+        t[0] = sizeof(t[0]) == 2 ? (uint32_t)((1u << 6) | in[0]) : (uint32_t)in[0];
         log = 0;
         return 1;
     case 0:  // predefined
@@ -984,7 +1027,8 @@ template <bool kRing, class E, class W>
 RPZ_COLD int64_t block(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out, uint64_t vstart, uint64_t pstart,
                        uint64_t op, uint64_t cap, uint64_t tail) {
     if (n >= kBlockMax) return RPZ_FAIL(-1);
-    constexpr bool kLdsWs = E::kInlineBlocks;  // the wave decoders keep Ws in LDS
+    // the wave decoders keep Ws in LDS, with the per-state baseline tables
+    constexpr bool kLdsWs = E::kInlineBlocks && W::kHasX;
     Lit lit;
 #if RPZ_PROF
     const uint64_t c0 = RPZ_CLK();
@@ -1018,13 +1062,13 @@ RPZ_COLD int64_t block(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out,
         }
         if (p + 1 > iend) return RPZ_FAIL(-1);
         const uint32_t modes = *p++;
-        int64_t h = seq_table(w, modes >> 6, 0, p, (uint64_t)(iend - p), kLdsWs);
+        int64_t h = seq_table<kLdsWs>(w, modes >> 6, 0, p, (uint64_t)(iend - p));
         if (h < 0) return RPZ_FAIL(-1);
         p += h;
-        h = seq_table(w, (modes >> 4) & 3, 1, p, (uint64_t)(iend - p), kLdsWs);
+        h = seq_table<kLdsWs>(w, (modes >> 4) & 3, 1, p, (uint64_t)(iend - p));
         if (h < 0) return RPZ_FAIL(-1);
         p += h;
-        h = seq_table(w, (modes >> 2) & 3, 2, p, (uint64_t)(iend - p), kLdsWs);
+        h = seq_table<kLdsWs>(w, (modes >> 2) & 3, 2, p, (uint64_t)(iend - p));
         if (h < 0) return RPZ_FAIL(-1);
         p += h;
     }
@@ -1041,10 +1085,17 @@ RPZ_COLD int64_t block(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out,
         uint32_t sOF = (uint32_t)read_bits(b, w.of_log);
         uint32_t sML = (uint32_t)read_bits(b, w.ml_log);
         for (uint32_t k = 0; k < nbSeq; k++) {
-            const uint32_t eLL = w.ll[sLL], eML = w.ml[sML], eOF = w.of[sOF];
+            const uint32_t eLL = fse_cell(w.ll, w.ll_log, sLL), eML = fse_cell(w.ml, w.ml_log, sML),
+                           eOF = fse_cell(w.of, w.of_log, sOF);
             const uint32_t cLL = eLL & 0xFF, cML = eML & 0xFF;  // <= 35 / 52: FSE symbols are checked
-            const uint32_t xLL = kLdsWs ? w.llx[sLL] : (kLLBase[cLL] | ((uint32_t)kLLBits[cLL] << 24));
-            const uint32_t xML = kLdsWs ? w.mlx[sML] : (kMLBase[cML] | ((uint32_t)kMLBits[cML] << 24));
+            uint32_t xLL, xML;
+            if constexpr (kLdsWs) {
+                xLL = w.llx[sLL];
+                xML = w.mlx[sML];
+            } else {
+                xLL = kLLBase[cLL] | ((uint32_t)kLLBits[cLL] << 24);
+                xML = kMLBase[cML] | ((uint32_t)kMLBits[cML] << 24);
+            }
             const uint32_t cOF = eOF & 0xFF;
             const uint32_t llBase = xLL & 0xFFFFFF, mlBase = xML & 0xFFFFFF;
             const uint32_t llBits = xLL >> 24, mlBits = xML >> 24, ofBits = cOF;
@@ -1353,8 +1404,8 @@ RPC_HD int32_t uncompress_impl(E& em, const uint8_t* in, uint64_t n, uint8_t* ou
             }
             if (T != fend) return RPZ_FAIL(V_ERROR);
             if (h.csum) {
-                em.sync();  // the checksum reads the decoded bytes
-                if ((uint32_t)xxh64(out + fstart, T - fstart) != le32(f + ip)) return RPZ_FAIL(V_ERROR);
+                // the checksum reads the decoded bytes
+                if (!em.checksum(out + fstart, T - fstart, le32(f + ip))) return RPZ_FAIL(V_ERROR);
             }
             S += h.fcs;  // decoded straight into the staging buffer
             p += csize;
@@ -1447,8 +1498,7 @@ RPC_HD int32_t uncompress_impl(E& em, const uint8_t* in, uint64_t n, uint8_t* ou
                 if (cb != 0 && h.fcs != kUnknown && decoded != h.fcs) return RPZ_FAIL(V_ERROR);
                 if (h.csum) {
                     if (rem - ip < 4) break;
-                    em.sync();
-                    if ((uint32_t)xxh64(out + fstart, T - fstart) != le32(f + ip)) return RPZ_FAIL(V_ERROR);
+                    if (!em.checksum(out + fstart, T - fstart, le32(f + ip))) return RPZ_FAIL(V_ERROR);
                     ip += 4;
                 }
                 done = true;

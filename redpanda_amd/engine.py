@@ -31,13 +31,17 @@ class Engine:
     """One rpgpu context (one per Seastar shard x GPU in the reference's terms)."""
 
     def __init__(self, device: int = 0, max_decoded_batch: int = 0, walk_overlap: bool = True,
-                 decomp_ws_lanes: int = 0, walk_chunks: int = 0, blocks_per_cu: int = 0):
+                 decomp_ws_lanes: int = 0, walk_chunks: int = 0, blocks_per_cu: int = 0,
+                 zstd_split: bool = False):
         """walk_overlap: the record walk beside the checksums (the default; False sets
         RPGPU_OPT_NO_WALK_OVERLAP);
         decomp_ws_lanes: rpgpu_opts.decomp_ws_lanes (0: the default ceiling);
-        walk_chunks / blocks_per_cu: rpgpu_opts tuning fields (0: defaults)."""
+        walk_chunks / blocks_per_cu: rpgpu_opts tuning fields (0: defaults);
+        zstd_split: the split zstd decoder (RPGPU_OPT_ZSTD_SPLIT; off by default)."""
         self._lib = abi.lib()
-        opts = abi.Opts(abi.OPT_WALK_OVERLAP if walk_overlap else abi.OPT_NO_WALK_OVERLAP, 0, 0, max_decoded_batch, decomp_ws_lanes,
+        flags = (abi.OPT_WALK_OVERLAP if walk_overlap else abi.OPT_NO_WALK_OVERLAP) | \
+            (abi.OPT_ZSTD_SPLIT if zstd_split else 0)
+        opts = abi.Opts(flags, 0, 0, max_decoded_batch, decomp_ws_lanes,
                         walk_chunks, blocks_per_cu)
         self._ctx = self._lib.rpgpu_open(device, C.byref(opts))
         if not self._ctx:

@@ -219,7 +219,9 @@ def test_many_tiny_zstd_gzip(eng):
 
 
 def zstd_workspace_bytes(got):
-    """Output bytes past the slots (rounded to 256): the zstd lane workspaces."""
+    """Output bytes past the slots (rounded to 256): the zstd lane workspaces
+    (engines opened with zstd_split=False: the split decoder's literal and
+    record regions follow the workspaces)."""
     d = got["dres"]
     end = int((d["out_offset"].astype(np.int64) + d["out_cap"].astype(np.int64))[d["out_cap"] > 0].max(initial=0))
     return got["out_bytes"] - ((end + 255) & ~255) if got["out_bytes"] > end else 0
@@ -229,14 +231,15 @@ def test_few_workspace_lanes():
     """rpgpu_opts.decomp_ws_lanes = 256: a mixed arena with 6,000 zstd / gzip
     batches still decodes exactly as the oracle, each of the 256 workspace
     lanes taking ~20 frames in turn; the plan's output bytes hold 256 zstd
-    workspaces, the scratch only gzip's."""
+    workspaces, the scratch only gzip's (the one-lane zstd decoder: the split
+    decoder off)."""
     from redpanda_amd import abi, engine
 
     spec = engine.make_spec(seed=0x5EED0078, partitions=32, codec_mix=(1 << 4) | (1 << 1) | (1 << 3),
                             body_min=100, body_max=20_000, ops=abi.OPS_PRODUCE | abi.OP_DECOMP,
                             payload=abi.PAYLOAD_TEXT, corrupt_ppm=5_000, corrupt_mask=0x3FF)
     data, descs = engine.build_arena(spec, 9000)
-    with engine.Engine(0, decomp_ws_lanes=256) as e:
+    with engine.Engine(0, decomp_ws_lanes=256, zstd_split=False) as e:
         n = 200_000
         assert e.decomp_scratch_bytes(n) < abi.lib().rpgpu_decomp_scratch_bytes(n)
         got = e.decompress_arena(data, descs)
@@ -247,12 +250,15 @@ def test_few_workspace_lanes():
     assert ws % 256 == 0 and 8 << 10 < ws // 256 < 32 << 10, ws
 
 
-def test_zstd_workspaces_follow_the_plan(eng):
+def test_zstd_workspaces_follow_the_plan():
     """the zstd lane workspaces sit after the output slots,
     one per zstd lane batch the plan found (up to the cap): an LZ4 / snappy
     arena's output is its slots alone and the scratch holds no zstd workspace;
-    k zstd batches add k workspaces; every batch decodes as the oracle."""
-    from redpanda_amd import abi
+    k zstd batches add k workspaces; every batch decodes as the oracle (the
+    one-lane zstd decoder: the split decoder off)."""
+    from redpanda_amd import abi, engine
+
+    eng = engine.Engine(0, zstd_split=False)
 
     assert abi.lib().rpgpu_decomp_scratch_bytes(131072) < 1 << 30  # was ~2.6 GB with them
     rng = np.random.default_rng(29)
@@ -273,6 +279,7 @@ def test_zstd_workspaces_follow_the_plan(eng):
         else:
             assert ws % k == 0, (ws, k)
             per.append(ws // k)
+    eng.close()
     assert per[0] == per[1] and 8 << 10 < per[0] < 32 << 10, per
 
 
@@ -507,3 +514,52 @@ def test_split_fallback_below_wave_size(eng):
     got = eng.decompress_arena(data, descs)
     want = compare(got, data, descs)
     assert want["verdicts"][0] == abi.V_DECOMP_ERROR and want["verdicts"][1] == abi.V_OK
+
+
+@pytest.mark.parametrize("case", ["tiny", "mixed", "c4", "mutated"])
+def test_zstd_split_decoder(case):
+    """The split zstd decoder (rpgpu_zseq.h: A1 literal sections with Huffman
+    tables in LDS, A2 the restatement's decisions writing copy records, B the
+    records executed) against the oracle, and against the one-lane decoder
+    (without RPGPU_OPT_ZSTD_SPLIT) byte for byte on the same arena: verdicts,
+    decoded lengths, rewritten batches, index.  Cases: many tiny bodies (more
+    batches than the split kernels' lanes), mixed sizes up to the lane / wave
+    boundary with 1 % corruption, the C4 shape (64 x 1 KiB text records at
+    level 3), and mutated payloads (verdicts decided by A2 on corrupt
+    frames)."""
+    from redpanda_amd import abi, engine
+
+    kw = dict(ops=abi.OPS_PRODUCE | abi.OP_DECOMP, payload=abi.PAYLOAD_TEXT)
+    if case == "tiny":
+        spec = engine.make_spec(seed=0x5EED0A01, partitions=64, codec_mix=1 << 4, body_min=60, body_max=500,
+                                corrupt_ppm=10_000, corrupt_mask=0x3FF, **kw)
+        n = 120_000
+    elif case == "mixed":
+        spec = engine.make_spec(seed=0x5EED0A02, partitions=64, codec_mix=(1 << 4) | (1 << 3), body_min=7,
+                                body_max=300_000, corrupt_ppm=10_000, corrupt_mask=0x3FF, **kw)
+        n = 6000
+    elif case == "c4":
+        spec = engine.make_spec(seed=0x5EED0A03, partitions=4096, records_per_batch=64, key_len=16, value_len=999,
+                                codec=4, **kw)
+        n = 4096
+    else:
+        spec = engine.make_spec(seed=0x5EED0A04, partitions=64, codec_mix=1 << 4, body_min=100, body_max=60_000,
+                                corrupt_ppm=200_000, corrupt_mask=0x200, **kw)
+        n = 6000
+    data, descs = engine.build_arena(spec, n)
+    with engine.Engine(0, zstd_split=True) as e:
+        got = e.decompress_arena(data, descs)
+    with engine.Engine(0) as e:
+        one = e.decompress_arena(data, descs)
+    for f in ("dres", "out_descs", "out_results"):
+        assert np.array_equal(got[f].view(np.uint8), one[f].view(np.uint8)), f
+    ok = np.nonzero(got["dres"]["verdict"] == abi.V_OK)[0]
+    for i in ok:
+        a = int(got["dres"]["out_offset"][i])
+        m = 61 + int(got["dres"]["out_len"][i])
+        assert np.array_equal(got["out"][a:a + m], one["out"][a:a + m]), f"batch {i}"
+    compare(got, data, descs, nthreads=8)
+    v, codec = got["dres"]["verdict"], got["dres"]["codec"]
+    assert ((v == abi.V_OK) & (codec == 4)).sum() > n // 4
+    if case == "mutated":
+        assert ((v != abi.V_OK) & (codec == 4)).sum() > 20
