@@ -294,8 +294,12 @@ RPC_HD void win_load(InWin& W, const uint8_t* in, int64_t p) {
     W.pos = p;
 }
 // dword q (0..8; 8 reads as 0) of the window: selects, not an indexed array
-// (an array would be placed in scratch memory on the device)
-RPC_HD uint32_t win_dword(const InWin& W, uint32_t q) {
+// (an array would be placed in scratch memory on the device).  By value: a
+// reference took the window's address, and the device compiler kept it in a
+// private array that it promoted to LDS -- 40 B per lane, 10 KiB per snappy
+// part workgroup, which then could not be resident beside the zstd wave
+// decoder's LDS workspaces (C5, profiles/r5/NOTES.md)
+RPC_HD uint32_t win_dword(const InWin W, uint32_t q) {
     const uint32_t a = (q & 1) ? W.w1 : W.w0, b = (q & 1) ? W.w3 : W.w2;
     const uint32_t c = (q & 1) ? W.w5 : W.w4, d = (q & 1) ? W.w7 : W.w6;
     const uint32_t lo = (q & 2) ? b : a, hi = (q & 2) ? d : c;

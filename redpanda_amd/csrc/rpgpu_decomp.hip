@@ -803,7 +803,9 @@ __global__ void decomp_ws_kernel(uint32_t* __restrict__ counter, uint32_t cap, u
     counter[21] = (uint32_t)(loff >> 32);
     counter[22] = (uint32_t)roff;
     counter[23] = (uint32_t)(roff >> 32);
-    if (out_bytes) *out_bytes = lanes ? roff + (cnt64(counter, 18) + 16) * 8 : slots;
+    // no batch planned for the split decoder (it is off, or no body qualified): no regions
+    const bool split = cnt64(counter, 18) != 0;
+    if (out_bytes) *out_bytes = split ? roff + (cnt64(counter, 18) + 16) * 8 : ws_end;
 }
 
 // One batch body through the codec restatement, bytes produced by the wave.
