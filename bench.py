@@ -375,8 +375,9 @@ def main() -> int:
                     help="the record walk beside the checksums (auto: the library default, on; "
                          "off: RPGPU_OPT_NO_WALK_OVERLAP)")
     ap.add_argument("--blocks-per-cu", type=int, default=0, help="rpgpu_opts.blocks_per_cu (tuning; 0 = default)")
-    ap.add_argument("--zstd-split", action="store_true",
-                    help="zstd through the split decoder (RPGPU_OPT_ZSTD_SPLIT; A/B measurements)")
+    ap.add_argument("--zstd-split", default="off", choices=["off", "lds", "fused"],
+                    help="zstd lane bodies through the split decoder (lds: RPGPU_OPT_ZSTD_SPLIT, fused: "
+                         "RPGPU_OPT_ZSTD_FUSED; A/B measurements)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only: launcher, gloo rendezvous, sharding and the summary gather, no engine")
     args = ap.parse_args()
@@ -416,7 +417,7 @@ def main() -> int:
     # of serial validate-then-walk, C2 ~9 % faster; profiles/r4/NOTES.md r4i / r4j)
     overlap = args.overlap != "off"
     eng = engine.Engine(local, walk_overlap=overlap, decomp_ws_lanes=cfg.get("ws_lanes", 0),
-                        walk_chunks=args.walk_chunks, blocks_per_cu=args.blocks_per_cu, zstd_split=args.zstd_split)
+                        walk_chunks=args.walk_chunks, blocks_per_cu=args.blocks_per_cu, zstd_split=False if args.zstd_split == "off" else args.zstd_split)
     chunks, P_total, part_shift, (plo, phi) = rank_chunks(cfg, rank, world, scaling, args.batches)
     n = sum(m for _, m in chunks)
 

@@ -200,6 +200,10 @@ typedef struct rpgpu_rp_header {
  * executed; rpgpu_zseq.h) instead of the one-lane decoder (tables in HBM).
  * Same verdicts and bytes; off by default (slower on C4 so far). */
 #define RPGPU_OPT_ZSTD_SPLIT 4u
+/* RPGPU_OPT_ZSTD_FUSED: the one-lane decoder's entropy stages (tables in HBM)
+ * writing copy records, then the split decoder's executor (rpgpu_zseq.h
+ * RecEmit + exec_lane).  Same verdicts and bytes. */
+#define RPGPU_OPT_ZSTD_FUSED 8u
 
 typedef struct rpgpu_opts {
     uint32_t flags;        /* RPGPU_OPT_* */

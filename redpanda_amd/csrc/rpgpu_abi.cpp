@@ -50,12 +50,12 @@ hipError_t launch_sets_run(const rpgpu_batch_desc* d_sets, uint32_t n, const uin
                            int grid, hipStream_t s, const Overlap* ov);
 hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                               const rpgpu_batch_result* d_vres, uint64_t* d_out_bytes, void* d_scratch,
-                              uint64_t max_decoded, uint32_t ws_cap, bool zsplit, hipStream_t s);
+                              uint64_t max_decoded, uint32_t ws_cap, uint32_t zmode, hipStream_t s);
 hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                              const rpgpu_batch_result* d_vres, rpgpu_decomp_result* d_dres, uint8_t* d_out,
                              uint64_t out_cap, rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_vres2,
                              rpgpu_record_index* d_index, uint64_t index_cap, uint64_t* d_index_used,
-                             void* d_scratch, const uint32_t* d_tables, int grid, uint32_t ws_cap, hipStream_t s,
+                             void* d_scratch, const uint32_t* d_tables, int grid, uint32_t ws_cap, uint32_t zmode, hipStream_t s,
                              const Overlap* ov, const DecompStreams* ds);
 hipError_t launch_uncompress_bound(uint32_t codec, const uint8_t* d_in, uint64_t n, uint64_t* d_res,
                                    hipStream_t s);
@@ -159,7 +159,7 @@ struct rpgpu_ctx {
     bool busy = false;  // one in-flight submission per context (shard-owned)
     uint64_t max_decoded = RPGPU_DEFAULT_MAX_DECODED_BATCH;  // opts.max_decoded_batch
     uint32_t ws_lanes = 0;  // opts.decomp_ws_lanes (0: the default ceiling)
-    bool zsplit = false;    // the split zstd decoder (RPGPU_OPT_ZSTD_SPLIT)
+    uint32_t zmode = 0;     // zstd lane bodies: 0 one-lane, 1 split (LDS), 2 fused + executor
     int efd = -1;       // rpgpu_eventfd: signalled by a host function after each stage
     std::string err;
 };
@@ -238,7 +238,7 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
     // the walk of chunk k beside the checksums of chunk k + 1:
     // on unless RPGPU_OPT_NO_WALK_OVERLAP
     const bool want_overlap = !(opts && (opts->flags & RPGPU_OPT_NO_WALK_OVERLAP));
-    c->zsplit = opts && (opts->flags & RPGPU_OPT_ZSTD_SPLIT);
+    c->zmode = !opts ? 0u : (opts->flags & RPGPU_OPT_ZSTD_SPLIT) ? 1u : (opts->flags & RPGPU_OPT_ZSTD_FUSED) ? 2u : 0u;
     if (!want_overlap) c->have_overlap = false;
     std::vector<uint32_t> t(rpgpu::kTableWords);
     rpgpu::build_tables(t.data());
@@ -481,7 +481,7 @@ int32_t rpgpu_decomp_plan_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, 
     if (!c || (n && (!d_descs || !d_data || !d_results || !d_scratch))) return RPGPU_EINVAL;
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     hipError_t e = rpgpu::launch_decomp_plan(d_descs, n, d_data, d_results, d_out_bytes, d_scratch,
-                                              c->max_decoded, c->ws_lanes, c->zsplit, s);
+                                              c->max_decoded, c->ws_lanes, c->zmode, s);
     if (e != hipSuccess) return fail(c, e, "decomp plan launch");
     return RPGPU_OK;
 }
@@ -498,7 +498,7 @@ int32_t rpgpu_decomp_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, u
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
     hipError_t e = rpgpu::launch_decomp_run(d_descs, n, d_data, d_results, d_dres, d_out, out_cap, d_out_descs,
                                             d_out_results, d_index, d_index ? index_cap : 0, d_index_used,
-                                            d_scratch, c->d_tables, c->grid, c->ws_lanes, s,
+                                            d_scratch, c->d_tables, c->grid, c->ws_lanes, c->zmode, s,
                                             c->have_overlap ? &c->overlap : nullptr,
                                             c->have_dstreams ? &c->dstreams : nullptr);
     if (e != hipSuccess) return fail(c, e, "decomp run launch");

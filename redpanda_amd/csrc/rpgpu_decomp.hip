@@ -765,6 +765,59 @@ __global__ __launch_bounds__(RPZS_WG) void zseq_seq_kernel(
     }
 }
 
+// A1 + A2 fused: one lane per planned batch with the one-lane decoder's
+// workspace in HBM (the lane workspaces after the output slots, as
+// ws_lane_kernel's), Huffman literals into the literal region, copies as
+// records.  Decides the verdict and length, or hands the batch back.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_WS_WAVES))) void zseq_fused_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data,
+    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
+    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
+    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
+    rpgpu_batch_desc* __restrict__ out_descs, const uint32_t* __restrict__ counter,
+    const uint32_t* __restrict__ zlist, uint32_t* __restrict__ flag, const uint64_t* __restrict__ lits,
+    const uint64_t* __restrict__ bs_l, const uint32_t* __restrict__ szl, const uint64_t* __restrict__ recs,
+    const uint64_t* __restrict__ bs_r, const uint32_t* __restrict__ szr) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t cnt = counter[7];
+    const uint32_t lanes = counter[10] < gridDim.x * blockDim.x ? counter[10] : gridDim.x * blockDim.x;
+    if (g >= lanes) return;
+    const uint64_t ws_off = cnt64(counter, 8), loff = cnt64(counter, 20), roff = cnt64(counter, 22);
+    rpzstd::Ws& w = reinterpret_cast<rpzstd::Ws*>(out + ws_off)[g];
+    const bool fits = roff + (cnt64(counter, 18) + 16) * 8 <= out_cap;
+    for (uint32_t k = g; k < cnt; k += lanes) {
+        const uint32_t f = flag[k];
+        if (!(f & kZPlanned)) continue;
+        if (!fits) {
+            flag[k] = kZPlanned | kZBack;
+            continue;
+        }
+        const uint32_t i = zlist[k];
+        const rpgpu_batch_desc d = descs[i];
+        const rpgpu_batch_result v = vres[i];
+        uint64_t sz = slot[i];
+        const uint64_t off = block_base[i / kScanBlock] + local[i];
+        int32_t verdict = RPGPU_V_SKIPPED;
+        uint64_t len = 0;
+        uint32_t nf = kZPlanned;
+        if (plan_slot(sz, off, out_cap, verdict, len)) {
+            rpzstd::RecEmit em{{nullptr, -1, out + loff + bs_l[k / kScanBlock] + lits[k], szl[k], 0,
+                                reinterpret_cast<uint64_t*>(out + roff) + bs_r[k / kScanBlock] + recs[k], 0, szr[k],
+                                nullptr, 0, false}};
+            verdict = rpzstd::uncompress<false>(em, data + d.offset + kHeaderSize, body_len(v), out + off + kHeaderSize,
+                                                sz - kHeaderSize - rpcodec::kSlack, &len, w);
+            em.put(rpzstd::rec_op(rpzstd::kOpEnd, 0));
+            if (em.fb || verdict == rpzstd::V_RING) {
+                flag[k] = kZPlanned | kZBack;
+                continue;
+            }
+            if (verdict == RPGPU_V_OK) nf |= kZExec;
+        }
+        finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
+        flag[k] = nf;
+    }
+}
+
 // B: the records of every batch A2 decided OK, one lane per batch
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_WAVES))) void zseq_exec_kernel(
     const uint32_t* __restrict__ counter, const uint32_t* __restrict__ zlist, const uint32_t* __restrict__ flag,
@@ -1027,7 +1080,7 @@ ZLaunch zseq_launch() {
 
 hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                               const rpgpu_batch_result* d_vres, uint64_t* d_out_bytes, void* d_scratch,
-                              uint64_t max_decoded, uint32_t ws_cap, bool zsplit, hipStream_t s) {
+                              uint64_t max_decoded, uint32_t ws_cap, uint32_t zmode, hipStream_t s) {
     if (n == 0) return d_out_bytes ? hipMemsetAsync(d_out_bytes, 0, sizeof(uint64_t), s) : hipSuccess;
     const Parts p = parts(d_scratch, n, ws_cap);
     const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
@@ -1049,7 +1102,7 @@ hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const
     // the split zstd decoder's reservations over the zstd lane list
     const ZParts z = zparts(d_scratch, n, ws_cap);
     zseq_plan_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, d_data, d_vres, p.slot, p.counter, p.wlist + 2 * (size_t)n,
-                                               z.flag, z.lits, z.recs, z.bs_l, z.bs_r, z.szl, z.szr, n, zsplit);
+                                               z.flag, z.lits, z.recs, z.bs_l, z.bs_r, z.szl, z.szr, n, zmode != 0);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = launch_block_scan(z.bs_l, nb, reinterpret_cast<uint64_t*>(p.counter + 16), s)) != hipSuccess) return e;
     if ((e = launch_block_scan(z.bs_r, nb, reinterpret_cast<uint64_t*>(p.counter + 18), s)) != hipSuccess) return e;
@@ -1062,8 +1115,8 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                              const rpgpu_batch_result* d_vres, rpgpu_decomp_result* d_dres, uint8_t* d_out,
                              uint64_t out_cap, rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_vres2,
                              rpgpu_record_index* d_index, uint64_t index_cap, uint64_t* d_index_used,
-                             void* d_scratch, const uint32_t* d_tables, int grid, uint32_t ws_cap, hipStream_t s,
-                             const Overlap* ov, const DecompStreams* ds) {
+                             void* d_scratch, const uint32_t* d_tables, int grid, uint32_t ws_cap, uint32_t zmode,
+                             hipStream_t s, const Overlap* ov, const DecompStreams* ds) {
     if (n == 0) return d_index_used ? hipMemsetAsync(d_index_used, 0, sizeof(uint64_t), s) : hipSuccess;
     const Parts p = parts(d_scratch, n, ws_cap);
     const uint32_t nblk = (n + 255) / 256;
@@ -1115,7 +1168,15 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     // the split decoder over the zstd lane batches it planned: A1 literals, A2
     // decisions + records, B execution; what A2 hands back, the one-lane decoder
     const ZParts z = zparts(d_scratch, n, ws_cap);
-    {
+    if (zmode == 2) {
+        zseq_fused_kernel<<<(zl + 255) / 256, 256, 0, s>>>(
+            d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.counter,
+            p.wlist + 2 * (size_t)n, z.flag, z.lits, z.bs_l, z.szl, z.recs, z.bs_r, z.szr);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        zseq_exec_kernel<<<(zl + 255) / 256, 256, 0, s>>>(p.counter, p.wlist + 2 * (size_t)n, z.flag, z.recs, z.bs_r,
+                                                         p.local, p.block_sum, d_out);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    } else if (zmode == 1) {
 #ifdef RPZS_HBM_WS
         const uint32_t zl_n = n < RPZ_LANES ? n : RPZ_LANES;
         const ZLaunch zq{(zl_n + 255) / 256, 256, 256};

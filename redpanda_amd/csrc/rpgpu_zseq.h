@@ -370,8 +370,11 @@ struct SeqEmit {
     }
     RPC_MF uint8_t* litbuf(uint8_t*, uint64_t, uint64_t size) {
         uint8_t* d = litbase + litcur;
+        if (litcur + size > litcap) {
+            fb = true;  // (RecEmit decodes nothing more)
+            return litbase;
+        }
         litcur += size;
-        if (litcur > litcap) fb = true;
         return d;
     }
     RPC_MF void litfill(uint8_t*, uint8_t, uint64_t) {}
@@ -399,6 +402,31 @@ struct SeqEmit {
     RPC_MF bool checksum(const uint8_t*, uint64_t, uint32_t) {
         fb = true;  // the bytes are not decoded here
         return true;
+    }
+};
+
+// ------------------------------------------------------------ A (fused)
+// A1 and A2 in one pass, with the one-lane decoder's workspace (rpzstd::Ws,
+// in HBM): Huffman tables read and streams decoded here, into the literal
+// region; copies written as records for B.  No section words.
+struct RecEmit : SeqEmit {
+    template <class W>
+    RPC_MF int64_t table(W& w, const uint8_t* src, uint64_t n) {
+        return huf_read_table(w, src, n);
+    }
+    template <class W>
+    RPC_MF bool huf1(const W& w, const uint8_t* src, uint64_t len, uint8_t* d, uint64_t n) {
+        return !fb && huf_stream(w, src, len, d, n, n, w.huf1_on != 0);
+    }
+    template <class W>
+    RPC_MF bool huf4(const W& w, const Huf4& a) {
+        if (fb) return false;
+        DirectEmit de;
+        return de.huf4(w, a);
+    }
+    RPC_MF void section_begin() {}
+    RPC_MF void litfill(uint8_t* d, uint8_t v, uint64_t n) {
+        if (!fb) fill_bytes(d, v, n);
     }
 };
 

@@ -315,6 +315,26 @@ void compare_split(const uint8_t* ip, size_t n, uint64_t cap, int32_t ev, uint64
         return;
     }
     n_split++;
+    // the fused form (RecEmit over the one-lane workspace) must make the same records' worth of bytes
+    {
+        static rpzstd::Ws fw;
+        std::vector<uint64_t> frec(pl.recs + 8);
+        Bytes flits(pl.lits + 64), fout(cap + rpcodec::kSlack);
+        rpzstd::RecEmit fe{{nullptr, -1, flits.data(), pl.lits, 0, frec.data(), 0, pl.recs, nullptr, 0, false}};
+        uint64_t flen = 0;
+        const int32_t fv = rpzstd::uncompress<false>(fe, ip, n, fout.data(), cap, &flen, fw);
+        fe.put(rpzstd::rec_op(rpzstd::kOpEnd, 0));
+        bool fsame = !fe.fb && fv == ev && (fv != 0 || flen == elen);
+        if (fsame && fv == 0) {
+            rpzstd::exec_lane(frec.data(), fout.data());
+            fsame = !memcmp(fout.data(), eout.data(), flen);
+        }
+        if (!fsame) {
+            fprintf(stderr, "case %ld: fused v=%d len=%llu fb=%d, one-lane v=%d len=%llu\n", n_cases, fv,
+                    (unsigned long long)flen, (int)fe.fb, ev, (unsigned long long)elen);
+            exit(1);
+        }
+    }
     bool same = sv == ev && (sv != 0 || slen == elen);
     if (same && sv == 0) {
         rpzstd::exec_lane(rec.data(), sout.data());

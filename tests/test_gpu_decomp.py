@@ -516,8 +516,9 @@ def test_split_fallback_below_wave_size(eng):
     assert want["verdicts"][0] == abi.V_DECOMP_ERROR and want["verdicts"][1] == abi.V_OK
 
 
+@pytest.mark.parametrize("mode", ["lds", "fused"])
 @pytest.mark.parametrize("case", ["tiny", "mixed", "c4", "mutated"])
-def test_zstd_split_decoder(case):
+def test_zstd_split_decoder(case, mode):
     """The split zstd decoder (rpgpu_zseq.h: A1 literal sections with Huffman
     tables in LDS, A2 the restatement's decisions writing copy records, B the
     records executed) against the oracle, and against the one-lane decoder
@@ -526,7 +527,8 @@ def test_zstd_split_decoder(case):
     batches than the split kernels' lanes), mixed sizes up to the lane / wave
     boundary with 1 % corruption, the C4 shape (64 x 1 KiB text records at
     level 3), and mutated payloads (verdicts decided by A2 on corrupt
-    frames)."""
+    frames).  Modes: the LDS split decoder (RPGPU_OPT_ZSTD_SPLIT) and the fused
+    entropy pass + executor (RPGPU_OPT_ZSTD_FUSED)."""
     from redpanda_amd import abi, engine
 
     kw = dict(ops=abi.OPS_PRODUCE | abi.OP_DECOMP, payload=abi.PAYLOAD_TEXT)
@@ -547,7 +549,7 @@ def test_zstd_split_decoder(case):
                                 corrupt_ppm=200_000, corrupt_mask=0x200, **kw)
         n = 6000
     data, descs = engine.build_arena(spec, n)
-    with engine.Engine(0, zstd_split=True) as e:
+    with engine.Engine(0, zstd_split=mode) as e:
         got = e.decompress_arena(data, descs)
     with engine.Engine(0) as e:
         one = e.decompress_arena(data, descs)
