@@ -378,6 +378,9 @@ def main() -> int:
     ap.add_argument("--zstd-split", default="off", choices=["off", "lds", "fused"],
                     help="zstd lane bodies through the split decoder (lds: RPGPU_OPT_ZSTD_SPLIT, fused: "
                          "RPGPU_OPT_ZSTD_FUSED; A/B measurements)")
+    ap.add_argument("--zstd-blocks", default="on", choices=["on", "off"],
+                    help="large zstd frames block-parallel (on, the default) or on the wave decoder only "
+                         "(off: RPGPU_OPT_ZSTD_WAVE_ONLY; A/B measurements)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU only: launcher, gloo rendezvous, sharding and the summary gather, no engine")
     args = ap.parse_args()
@@ -417,7 +420,8 @@ def main() -> int:
     # of serial validate-then-walk, C2 ~9 % faster; profiles/r4/NOTES.md r4i / r4j)
     overlap = args.overlap != "off"
     eng = engine.Engine(local, walk_overlap=overlap, decomp_ws_lanes=cfg.get("ws_lanes", 0),
-                        walk_chunks=args.walk_chunks, blocks_per_cu=args.blocks_per_cu, zstd_split=False if args.zstd_split == "off" else args.zstd_split)
+                        walk_chunks=args.walk_chunks, blocks_per_cu=args.blocks_per_cu, zstd_split=False if args.zstd_split == "off" else args.zstd_split,
+                        zstd_blocks=args.zstd_blocks == "on")
     chunks, P_total, part_shift, (plo, phi) = rank_chunks(cfg, rank, world, scaling, args.batches)
     n = sum(m for _, m in chunks)
 

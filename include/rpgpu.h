@@ -204,6 +204,14 @@ typedef struct rpgpu_rp_header {
  * writing copy records, then the split decoder's executor (rpgpu_zseq.h
  * RecEmit + exec_lane).  Same verdicts and bytes. */
 #define RPGPU_OPT_ZSTD_FUSED 8u
+/* RPGPU_OPT_ZSTD_WAVE_ONLY: zstd frames above the lane decoders' slots all go
+ * to the one-wave-per-frame decoder.  By default a large frame that is one
+ * complete frame without checksum or dictionary, of known content size that
+ * the decoder's ring holds whole, is decoded block-parallel (rpgpu_zblk.h:
+ * every block's literals and sequences at once, then the frame's repeat
+ * offsets resolved and its sequences executed by one wave).  Same verdicts
+ * and bytes either way. */
+#define RPGPU_OPT_ZSTD_WAVE_ONLY 16u
 
 typedef struct rpgpu_opts {
     uint32_t flags;        /* RPGPU_OPT_* */

@@ -26,6 +26,7 @@ OPT_WALK_OVERLAP = 1  # rpgpu_opts.flags: RPGPU_OPT_WALK_OVERLAP (the default)
 OPT_NO_WALK_OVERLAP = 2  # RPGPU_OPT_NO_WALK_OVERLAP
 OPT_ZSTD_SPLIT = 4  # RPGPU_OPT_ZSTD_SPLIT
 OPT_ZSTD_FUSED = 8  # RPGPU_OPT_ZSTD_FUSED
+OPT_ZSTD_WAVE_ONLY = 16  # RPGPU_OPT_ZSTD_WAVE_ONLY
 OP_RECRC = 32
 OPS_PRODUCE = OP_CRC | OP_HDRCRC | OP_PARSE | OP_INDEX
 

@@ -239,6 +239,7 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
     // on unless RPGPU_OPT_NO_WALK_OVERLAP
     const bool want_overlap = !(opts && (opts->flags & RPGPU_OPT_NO_WALK_OVERLAP));
     c->zmode = !opts ? 0u : (opts->flags & RPGPU_OPT_ZSTD_SPLIT) ? 1u : (opts->flags & RPGPU_OPT_ZSTD_FUSED) ? 2u : 0u;
+    if (opts && (opts->flags & RPGPU_OPT_ZSTD_WAVE_ONLY)) c->zmode |= 4u;  // kZModeNoBlk
     if (!want_overlap) c->have_overlap = false;
     std::vector<uint32_t> t(rpgpu::kTableWords);
     rpgpu::build_tables(t.data());

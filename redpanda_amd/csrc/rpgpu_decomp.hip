@@ -36,6 +36,7 @@
 #include "rpgpu_codec.h"
 #include "rpgpu_zstd.h"
 #include "rpgpu_zseq.h"
+#include "rpgpu_zblk.h"
 #include "rpgpu_wave.h"
 #include "rpgpu_inflate.h"
 
@@ -53,7 +54,10 @@ size_t validate_scratch_bytes(uint32_t n);
 namespace {
 // wave decoders in flight: 8 per CU (the zstd workspace takes ~19 KB of the
 // 160 KiB LDS) on 256 CUs; each owns a literal scratch buffer
-constexpr uint32_t kDecompWaves = 2048;
+#ifndef RPGPU_DECOMP_WAVES
+#define RPGPU_DECOMP_WAVES 2048
+#endif
+constexpr uint32_t kDecompWaves = RPGPU_DECOMP_WAVES;
 constexpr uint64_t kLitScratch = (128u << 10) + 256;  // ZSTD_BLOCKSIZE_MAX + slack
 // lane zstd / gzip decoders in flight, each with its workspace in HBM
 #ifndef RPZ_LANES
@@ -147,6 +151,34 @@ struct ZParts {
     uint32_t *szl, *szr;                   // the plan's literal bytes / records per entry
     uint32_t* sec;
 };
+// the block-parallel decoder of large zstd frames (rpgpu_zblk.h), after the
+// split decoder's state: per zstd wave list entry (the first kBlkFrames) its
+// frame record, then a pool of kBlkPool blocks and each block's entry
+constexpr uint32_t kBlkFrames = 16384, kBlkPool = 65536;
+struct ZbFrame {
+    uint32_t first, nblk;  // pool blocks; nblk 0: not planned (the wave decoder's)
+    uint64_t lits, recs;   // offsets in the literal / record regions
+    uint64_t fcs, bsm;
+};
+static_assert(sizeof(ZbFrame) == 40, "ZbFrame layout");
+uint32_t zb_frames(uint32_t n) { return n < kBlkFrames ? n : kBlkFrames; }
+size_t zblk_offset(uint32_t n, uint32_t cap) { return (zseq_offset(n, cap) + zseq_bytes(n) + 255) & ~(size_t)255; }
+size_t zblk_bytes(uint32_t n) {
+    return (size_t)zb_frames(n) * sizeof(ZbFrame) + (size_t)kBlkPool * (sizeof(rpzstd::Blk) + 4) + 256;
+}
+struct ZbParts {
+    ZbFrame* frames;
+    rpzstd::Blk* pool;
+    uint32_t* bframe;
+};
+ZbParts zbparts(void* p, uint32_t n, uint32_t cap) {
+    uint8_t* b = static_cast<uint8_t*>(p) + zblk_offset(n, cap);
+    ZbParts z;
+    z.pool = reinterpret_cast<rpzstd::Blk*>(b);
+    z.frames = reinterpret_cast<ZbFrame*>(z.pool + kBlkPool);
+    z.bframe = reinterpret_cast<uint32_t*>(z.frames + zb_frames(n));
+    return z;
+}
 ZParts zparts(void* p, uint32_t n, uint32_t cap) {
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
     uint8_t* b = static_cast<uint8_t*>(p) + zseq_offset(n, cap);
@@ -181,7 +213,7 @@ Parts parts(void* p, uint32_t n, uint32_t cap) {
 }
 }  // namespace
 
-size_t decomp_scratch_bytes(uint32_t n, uint32_t ws_cap) { return zseq_offset(n, ws_cap) + zseq_bytes(n); }
+size_t decomp_scratch_bytes(uint32_t n, uint32_t ws_cap) { return zblk_offset(n, ws_cap) + zblk_bytes(n); }
 
 // slots above this go to the wave decoders (a lane's serial decode of a
 // large body would hold up the whole launch)
@@ -209,6 +241,8 @@ constexpr uint64_t kOverCeiling = 1ull << 63;
 
 // the split zstd decoder's per-entry flags (zseq_*_kernel below)
 constexpr uint32_t kZPlanned = 1, kZBack = 2, kZExec = 4, kZOver = 8;
+// zmode: bits 0..1 the split decoder (0 off, 1 LDS, 2 fused), bit 2 large frames on the wave decoder only
+constexpr uint32_t kZModeNoBlk = 4;
 __device__ __forceinline__ uint64_t cnt64(const uint32_t* c, int k) {
     return (uint64_t)c[k] | ((uint64_t)c[k + 1] << 32);
 }
@@ -837,6 +871,174 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_
     }
 }
 
+// ------------------------------------------- block-parallel zstd (large frames)
+// (rpgpu_zblk.h).  Counters: [24..25] literal bytes, [26..27] records planned
+// (u64), [28] pool blocks reserved, [30..31] / [32..33] the literal / record
+// regions' offsets in the output buffer (after the split decoder's).
+__device__ __forceinline__ bool zb_fits(const uint32_t* counter, uint64_t out_cap) {
+    return cnt64(counter, 32) + (cnt64(counter, 26) + 16) * 8 <= out_cap;
+}
+
+// P: one lane per zstd wave list entry (the first kBlkFrames): the frame's
+// blocks counted, reserved in the pool and the regions, then recorded
+__global__ __launch_bounds__(256) void zblk_plan_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data,
+    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot, uint32_t* __restrict__ counter,
+    const uint32_t* __restrict__ wlist, ZbFrame* __restrict__ frames, rpzstd::Blk* __restrict__ pool,
+    uint32_t* __restrict__ bframe, uint32_t nframes, bool enabled) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nframes || k >= counter[2]) return;
+    ZbFrame f{0, 0, 0, 0, 0, 0};
+    const uint32_t i = wlist[k];
+    const rpgpu_batch_desc d = descs[i];
+    const rpgpu_batch_result v = vres[i];
+    const uint64_t sz = slot[i];
+    if (enabled && decomp_wanted(d, v) && v.codec == 4 && !(sz & kOverCeiling) && sz > lane_max(4)) {
+        const uint8_t* in = data + d.offset + kHeaderSize;
+        const uint64_t cap = sz - kHeaderSize - rpcodec::kSlack;
+        const rpzstd::BlkPlan pl = rpzstd::plan_blocks(in, body_len(v), cap, nullptr);
+        if (pl.ok && pl.nblk > 0) {
+            const uint32_t first = atomicAdd(counter + 28, pl.nblk);
+            if ((uint64_t)first + pl.nblk <= kBlkPool) {
+                f.first = first;
+                f.nblk = pl.nblk;
+                f.lits = atomicAdd(reinterpret_cast<unsigned long long*>(counter + 24), (unsigned long long)pl.lits);
+                f.recs = atomicAdd(reinterpret_cast<unsigned long long*>(counter + 26), (unsigned long long)pl.recs);
+                f.fcs = pl.fcs;
+                f.bsm = pl.bsm;
+                rpzstd::plan_blocks(in, body_len(v), cap, pool + first);
+                for (uint32_t j = 0; j < pl.nblk; j++) bframe[first + j] = k;
+            } else {
+                for (uint32_t j = first; j < kBlkPool; j++) bframe[j] = ~0u;  // a hole: no entry's
+            }
+        }
+    }
+    frames[k] = f;
+}
+
+// E1 + E2: one lane per task (block b's literals: task 2b, its sequences:
+// task 2b + 1), each lane's Huffman / FSE workspace in LDS
+union ZbWs {
+    rpzstd::HufWs h;
+    rpzstd::SeqWs s;
+};
+__global__ __launch_bounds__(64) void zblk_entropy_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data, const uint32_t* __restrict__ counter,
+    const uint32_t* __restrict__ wlist, const ZbFrame* __restrict__ frames, rpzstd::Blk* __restrict__ pool,
+    const uint32_t* __restrict__ bframe, uint8_t* __restrict__ out, uint64_t out_cap, uint32_t per_wg) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+    const uint32_t l = threadIdx.x;
+    if (l >= per_wg || !zb_fits(counter, out_cap)) return;
+    ZbWs& w = reinterpret_cast<ZbWs*>(dyn_lds)[l];
+    const uint32_t used = counter[28] < kBlkPool ? counter[28] : kBlkPool;
+    const uint64_t loff = cnt64(counter, 30), roff = cnt64(counter, 32);
+    const uint32_t lanes = gridDim.x * per_wg;
+    for (uint32_t t = blockIdx.x * per_wg + l; t < 2 * used; t += lanes) {
+        const uint32_t b = t >> 1, k = bframe[b];
+        if (k == ~0u) continue;
+        const ZbFrame f = frames[k];
+        const uint8_t* in = data + descs[wlist[k]].offset + kHeaderSize;
+        const uint32_t j = b - f.first;
+        if (t & 1)
+            pool[b].e2 = rpzstd::blk_sequences(in, pool + f.first, j, reinterpret_cast<uint64_t*>(out + roff) + f.recs, w.s);
+        else
+            pool[b].e1 = rpzstd::blk_literals(in, pool + f.first, j, out + loff + f.lits, w.h);
+    }
+}
+
+// R + X: one wave per planned frame.  Per block: 64 records at a time, the
+// repeat offsets resolved by a wave scan (rpzstd::RepFn), the positions by
+// scans of the lengths, every check of ZSTD_execSequence by the lanes at once;
+// a group that passes is executed (rpwave::exec_seqs).  Verdict and length
+// as rpzstd::uncompress decides them for such a frame (rpgpu_zblk.h).
+__device__ __forceinline__ uint32_t shfl_up32(uint32_t x, int s) { return (uint32_t)__shfl_up((int)x, s, 64); }
+__device__ int32_t zblk_run(const uint8_t* in, const ZbFrame& f, const rpzstd::Blk* __restrict__ blk,
+                            const uint8_t* lits, const uint64_t* recs, uint8_t* out, uint64_t cap, uint64_t* out_len,
+                            uint32_t lid) {
+    using namespace rpzstd;
+    uint64_t T = 0;
+    uint32_t s0 = 1, s1 = 4, s2 = 8;
+    *out_len = 0;
+    for (uint32_t j = 0; j < f.nblk; j++) {
+        const Blk b = blk[j];
+        const uint64_t room = f.fcs - T;
+        if (b.type != 2) {
+            if (b.size > room || (b.type == 1 && b.size > f.bsm) || T + b.size > cap) return V_ERROR;
+            if (b.type == 0) rpwave::coop_copy(out + T, in + b.in_off, b.size, lid);
+            else rpwave::coop_fill(out + T, in[b.in_off], b.size, lid);
+            T += b.size;
+            continue;
+        }
+        if (b.e1 < 0 || b.e2 < 0) return V_ERROR;
+        if (b.lit_type != 0 && b.lit_size > cap - T) return V_ERROR;
+        const uint64_t lim = room < cap - T ? room : cap - T;
+        const uint64_t oend = T + lim;
+        const uint8_t* const lb = b.lit_type == 0 ? in + b.in_off + b.lit_hs : lits + b.lit_out;
+        const uint64_t* const rec = recs + b.rec_out;
+        uint64_t o = T, lp = 0;
+        for (uint32_t g = 0; g < b.nseq; g += 64) {
+            const uint32_t q = g + lid;
+            const bool valid = q < b.nseq;
+            const uint64_t x = valid ? rec[q] : 0;
+            const uint64_t ll = valid ? (x >> 28) & kLenMask : 0, ml = valid ? x >> 46 : 0;
+            RepFn F = valid ? rep_fn(x) : RepFn{rep_ref(0, 0), rep_ref(1, 0), rep_ref(2, 0)};
+#pragma unroll
+            for (int st = 1; st < 64; st <<= 1) {
+                const RepFn y{shfl_up32(F.c0, st), shfl_up32(F.c1, st), shfl_up32(F.c2, st)};
+                if (lid >= (uint32_t)st) F = rep_then(y, F);
+            }
+            const uint64_t offset = rep_at(F.c0, s0, s1, s2);
+            const uint64_t tot = ll + ml;
+            const uint64_t inc = rpwave::wave_scan_incl(tot, lid), linc = rpwave::wave_scan_incl(ll, lid);
+            const uint64_t oo = o + inc - tot, lq = lp + linc - ll;
+            const bool bad = valid && (oo > oend || tot > oend - oo || lq + ll > b.lit_size || offset > oo + ll);
+            if (rpwave::ballot(bad)) return V_ERROR;
+            rpwave::exec_seqs(out + o, valid, lb + lq, ll, ml, offset, lid);
+            const uint32_t t0 = rep_at(F.c0, s0, s1, s2), t1 = rep_at(F.c1, s0, s1, s2), t2 = rep_at(F.c2, s0, s1, s2);
+            s0 = __builtin_amdgcn_readlane(t0, 63);
+            s1 = __builtin_amdgcn_readlane(t1, 63);
+            s2 = __builtin_amdgcn_readlane(t2, 63);
+            o += rpwave::readlane64(inc, 63);
+            lp += rpwave::readlane64(linc, 63);
+        }
+        const uint64_t last = b.lit_size - lp;
+        if (last > oend - o) return V_ERROR;
+        rpwave::coop_copy(out + o, lb + lp, last, lid);
+        o += last;
+        if (o - T > f.bsm) return V_ERROR;
+        T = o;
+    }
+    const Blk e = blk[f.nblk - 1];
+    if (T != f.fcs && !(e.type == 0 && e.size == 0)) return V_ERROR;
+    *out_len = T;
+    return V_OK;
+}
+__global__ __launch_bounds__(64) void zblk_exec_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data,
+    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
+    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
+    rpgpu_decomp_result* __restrict__ dres, uint8_t* out, uint64_t out_cap,
+    rpgpu_batch_desc* __restrict__ out_descs, const uint32_t* __restrict__ counter, const uint32_t* __restrict__ wlist,
+    const ZbFrame* __restrict__ frames, const rpzstd::Blk* __restrict__ pool) {
+    const uint32_t k = blockIdx.x, lid = lane_id();
+    if (k >= counter[2]) return;
+    const ZbFrame f = frames[k];
+    if (f.nblk == 0 || !zb_fits(counter, out_cap)) return;
+    const uint32_t i = wlist[k];
+    const rpgpu_batch_desc d = descs[i];
+    const rpgpu_batch_result v = vres[i];
+    uint64_t sz = slot[i];
+    const uint64_t off = block_base[i / kScanBlock] + local[i];
+    int32_t verdict = RPGPU_V_SKIPPED;
+    uint64_t len = 0;
+    if (plan_slot(sz, off, out_cap, verdict, len)) {
+        verdict = zblk_run(data + d.offset + kHeaderSize, f, pool + f.first, out + cnt64(counter, 30) + f.lits,
+                           reinterpret_cast<const uint64_t*>(out + cnt64(counter, 32)) + f.recs, out + off + kHeaderSize,
+                           sz - kHeaderSize - rpcodec::kSlack, &len, lid);
+    }
+    if (lid == 0) finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
+}
+
 // After the plan's scan: the zstd lane workspaces go after the output slots
 // (256-byte aligned), min(listed zstd lane batches, cap) of them; the plan's
 // output bytes include them.  counter[8..9] = their offset, [10] = lanes.
@@ -858,7 +1060,16 @@ __global__ void decomp_ws_kernel(uint32_t* __restrict__ counter, uint32_t cap, u
     counter[23] = (uint32_t)(roff >> 32);
     // no batch planned for the split decoder (it is off, or no body qualified): no regions
     const bool split = cnt64(counter, 18) != 0;
-    if (out_bytes) *out_bytes = split ? roff + (cnt64(counter, 18) + 16) * 8 : ws_end;
+    const uint64_t send = split ? roff + (cnt64(counter, 18) + 16) * 8 : ws_end;
+    // the block-parallel decoder's literal and record regions, likewise
+    const uint64_t bl = (send + 255) & ~(uint64_t)255;
+    const uint64_t br = (bl + cnt64(counter, 24) + 64 + 255) & ~(uint64_t)255;
+    counter[30] = (uint32_t)bl;
+    counter[31] = (uint32_t)(bl >> 32);
+    counter[32] = (uint32_t)br;
+    counter[33] = (uint32_t)(br >> 32);
+    const bool blk = counter[28] != 0;
+    if (out_bytes) *out_bytes = blk ? br + (cnt64(counter, 26) + 16) * 8 : send;
 }
 
 // One batch body through the codec restatement, bytes produced by the wave.
@@ -893,7 +1104,8 @@ __global__ __launch_bounds__(64) void decomp_wave_kernel(
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
     rpgpu_decomp_result* __restrict__ dres, uint8_t* out, uint64_t out_cap,
     rpgpu_batch_desc* __restrict__ out_descs, uint32_t* counter, uint8_t* lit_scratch,
-    const uint32_t* __restrict__ list, const uint32_t* __restrict__ list_len) {
+    const uint32_t* __restrict__ list, const uint32_t* __restrict__ list_len, const ZbFrame* __restrict__ zb,
+    const uint32_t* __restrict__ cbase) {
     // the zstd workspace: dynamic LDS, sizeof(Ws) for the zstd instance, none for LZ
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
     rpzstd::Ws& ws = *reinterpret_cast<rpzstd::Ws*>(dyn_lds);
@@ -902,11 +1114,14 @@ __global__ __launch_bounds__(64) void decomp_wave_kernel(
     if (len_list == 0) return;
     rpwave::WaveEmit em;
     em.init(lit_scratch + (uint64_t)blockIdx.x * kLitScratch);
+    // frames the block-parallel decoder took (zblk_exec_kernel): not here
+    const bool zb_on = zb != nullptr && zb_fits(cbase, out_cap);
     for (;;) {
         uint32_t k = 0;
         if (lid == 0) k = atomicAdd(counter, 1u);
         k = __builtin_amdgcn_readfirstlane(k);
         if (k >= len_list) break;
+        if (zb_on && k < kBlkFrames && zb[k].nblk != 0) continue;
         const uint32_t i = list[k];
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
@@ -1078,6 +1293,28 @@ ZLaunch zseq_launch() {
     return z;
 }
 
+// the block-parallel decoder's entropy lanes: as the split decoder's, one
+// ZbWs (Huffman or FSE tables) per lane in LDS
+struct ZbLaunch {
+    uint32_t grid, lanes;
+};
+ZbLaunch zblk_launch() {
+    static ZbLaunch z{0, 0};
+    if (z.grid) return z;
+    int dev = 0, cus = 0, lds = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
+    if (lds < (int)sizeof(ZbWs)) lds = (int)sizeof(ZbWs);
+    size_t k = (size_t)lds / RPZS_WAVES / sizeof(ZbWs);
+    k = k > 64 ? 64 : (k < 1 ? 1 : k);
+    ZbLaunch t{(uint32_t)((cus > 0 ? cus : 256) * RPZS_WAVES), (uint32_t)k};
+    hipFuncSetAttribute(reinterpret_cast<const void*>(zblk_entropy_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)(t.lanes * sizeof(ZbWs)));
+    z = t;
+    return z;
+}
+
 hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                               const rpgpu_batch_result* d_vres, uint64_t* d_out_bytes, void* d_scratch,
                               uint64_t max_decoded, uint32_t ws_cap, uint32_t zmode, hipStream_t s) {
@@ -1099,10 +1336,19 @@ hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const
     if (e != hipSuccess) return e;
     decomp_counters_kernel<<<1, 64, 0, s>>>(p.counter, 0);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    // the block-parallel decoder's frames among the zstd wave list (counters 24..29)
+    if ((e = hipMemsetAsync(p.counter + 24, 0, 6 * sizeof(uint32_t), s)) != hipSuccess) return e;
+    {
+        const ZbParts zb = zbparts(d_scratch, n, ws_cap);
+        zblk_plan_kernel<<<(zb_frames(n) + 255) / 256, 256, 0, s>>>(d_descs, d_data, d_vres, p.slot, p.counter, p.wlist,
+                                                                   zb.frames, zb.pool, zb.bframe, zb_frames(n),
+                                                                   !(zmode & kZModeNoBlk));
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     // the split zstd decoder's reservations over the zstd lane list
     const ZParts z = zparts(d_scratch, n, ws_cap);
     zseq_plan_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, d_data, d_vres, p.slot, p.counter, p.wlist + 2 * (size_t)n,
-                                               z.flag, z.lits, z.recs, z.bs_l, z.bs_r, z.szl, z.szr, n, zmode != 0);
+                                               z.flag, z.lits, z.recs, z.bs_l, z.bs_r, z.szl, z.szr, n, (zmode & 3) != 0);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = launch_block_scan(z.bs_l, nb, reinterpret_cast<uint64_t*>(p.counter + 16), s)) != hipSuccess) return e;
     if ((e = launch_block_scan(z.bs_r, nb, reinterpret_cast<uint64_t*>(p.counter + 18), s)) != hipSuccess) return e;
@@ -1143,10 +1389,22 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     if (ds) {
         if ((e = hipEventRecord(ds->parts, s)) != hipSuccess) return e;
     }
-    // zstd frames above kZstdLaneMaxSlot on the second stream (the wave decoder)
+    // zstd frames above kZstdLaneMaxSlot on the second stream: block-parallel
+    // (entropy stages per block, then one wave per frame), the rest by the wave decoder
+    const ZbParts zb = zbparts(d_scratch, n, ws_cap);
+    {
+        const ZbLaunch zq = zblk_launch();
+        zblk_entropy_kernel<<<zq.grid, 64, zq.lanes * sizeof(ZbWs), ws>>>(d_descs, d_data, p.counter, p.wlist, zb.frames,
+                                                                       zb.pool, zb.bframe, d_out, out_cap, zq.lanes);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        zblk_exec_kernel<<<zb_frames(n), 64, 0, ws>>>(d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
+                                                      out_cap, d_out_descs, p.counter, p.wlist, zb.frames, zb.pool);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     decomp_wave_kernel<kFamZstd><<<decomp_waves(n), 64, sizeof(rpzstd::Ws), ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
                                                                 p.block_sum, d_dres, d_out, out_cap, d_out_descs,
-                                                                p.counter + 1, p.lits, p.wlist, p.counter + 2);
+                                                                p.counter + 1, p.lits, p.wlist, p.counter + 2,
+                                                                zb.frames, p.counter);
     if (ds) {
         if ((e = hipStreamWaitEvent(ws, ds->parts, 0)) != hipSuccess) return e;
     }
@@ -1156,7 +1414,8 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     if ((e = hipGetLastError()) != hipSuccess) return e;
     decomp_wave_kernel<kFamLz><<<decomp_waves(n), 64, 0, ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
                                                               p.block_sum, d_dres, d_out, out_cap, d_out_descs,
-                                                              p.counter, p.lits, p.wlist + n, p.counter + 3);
+                                                              p.counter, p.lits, p.wlist + n, p.counter + 3, nullptr,
+                                                              nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t lzb = (n + 255) / 256;
     decomp_lane_kernel<3><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
@@ -1168,7 +1427,7 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     // the split decoder over the zstd lane batches it planned: A1 literals, A2
     // decisions + records, B execution; what A2 hands back, the one-lane decoder
     const ZParts z = zparts(d_scratch, n, ws_cap);
-    if (zmode == 2) {
+    if ((zmode & 3) == 2) {
         zseq_fused_kernel<<<(zl + 255) / 256, 256, 0, s>>>(
             d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.counter,
             p.wlist + 2 * (size_t)n, z.flag, z.lits, z.bs_l, z.szl, z.recs, z.bs_r, z.szr);
@@ -1176,7 +1435,7 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
         zseq_exec_kernel<<<(zl + 255) / 256, 256, 0, s>>>(p.counter, p.wlist + 2 * (size_t)n, z.flag, z.recs, z.bs_r,
                                                          p.local, p.block_sum, d_out);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-    } else if (zmode == 1) {
+    } else if ((zmode & 3) == 1) {
 #ifdef RPZS_HBM_WS
         const uint32_t zl_n = n < RPZ_LANES ? n : RPZ_LANES;
         const ZLaunch zq{(zl_n + 255) / 256, 256, 256};

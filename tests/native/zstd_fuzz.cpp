@@ -25,6 +25,7 @@
 #include "rpgpu.h"
 #include "rpgpu_zstd.h"
 #include "rpgpu_zseq.h"
+#include "rpgpu_zblk.h"
 #include "rpgpu_zstdc.h"
 
 extern "C" {
@@ -41,7 +42,8 @@ namespace {
 typedef std::vector<uint8_t> Bytes;
 std::mt19937_64 rng;
 uint64_t below(uint64_t n) { return n ? rng() % n : 0; }
-long n_cases = 0, n_ok = 0, n_rejected = 0, n_ring = 0, n_split = 0, n_split_fb = 0, n_split_no = 0;
+long n_cases = 0, n_ok = 0, n_rejected = 0, n_ring = 0, n_split = 0, n_split_fb = 0, n_split_no = 0,
+     n_blk = 0, n_blk_ok = 0;
 
 void fail(const char* what) {
     fprintf(stderr, "FAIL: %s\n", what);
@@ -358,6 +360,79 @@ void compare_split(const uint8_t* ip, size_t n, uint64_t cap, int32_t ev, uint64
     }
 }
 
+// The block-parallel path for large frames (rpgpu_zblk.h: plan, per-block
+// literals and sequences, serial resolve, execution) against the decoder's
+// final verdict, length and bytes, for every body it plans.
+void compare_blk(const uint8_t* ip, size_t n, uint64_t cap, int32_t ev, uint64_t elen, const Bytes& eout) {
+    static rpzstd::Blk blk[rpzstd::kBlkMax];
+    const rpzstd::BlkPlan pl = rpzstd::plan_blocks(ip, n, cap, blk);
+    if (!pl.ok) return;
+    n_blk++;
+    Bytes lits(pl.lits + 64);
+    for (auto& c : lits) c = (uint8_t)rng();
+    std::vector<uint64_t> rec(pl.recs + 8);
+    static rpzstd::HufWs hw;
+    static rpzstd::SeqWs sw;
+    // blocks in a shuffled order: each stage reads only the plan and its own block's sources
+    std::vector<uint32_t> order(pl.nblk);
+    for (uint32_t k = 0; k < pl.nblk; k++) order[k] = k;
+    for (uint32_t k = pl.nblk; k > 1; k--) std::swap(order[k - 1], order[below(k)]);
+    for (uint32_t k : order) blk[k].e1 = rpzstd::blk_literals(ip, blk, k, lits.data(), hw);
+    for (uint32_t k : order) blk[k].e2 = rpzstd::blk_sequences(ip, blk, k, rec.data(), sw);
+    std::vector<uint64_t> raw(rec.size());
+    memcpy(raw.data(), rec.data(), rec.size() * sizeof(uint64_t));
+    uint64_t len = 0;
+    const int32_t v = rpzstd::blk_resolve(blk, pl, rec.data(), cap, &len);
+    if (v == 0) {
+        // the device's resolution: 64 sequences at a time, a Hillis-Steele scan
+        // of the repeat-offset functions, must give the serial offsets
+        uint32_t s0 = 1, s1 = 4, s2 = 8;
+        for (uint32_t k = 0; k < pl.nblk; k++) {
+            const rpzstd::Blk& b = blk[k];
+            for (uint32_t g = 0; g < b.nseq; g += 64) {
+                const uint32_t m = b.nseq - g < 64 ? b.nseq - g : 64;
+                rpzstd::RepFn x[64];
+                for (uint32_t l = 0; l < 64; l++)
+                    x[l] = l < m ? rpzstd::rep_fn(raw[b.rec_out + g + l]) : rpzstd::RepFn{0u, 1u << 27, 2u << 27};
+                for (uint32_t st = 1; st < 64; st <<= 1) {
+                    rpzstd::RepFn y[64];
+                    for (uint32_t l = 0; l < 64; l++) y[l] = l >= st ? rpzstd::rep_then(x[l - st], x[l]) : x[l];
+                    for (uint32_t l = 0; l < 64; l++) x[l] = y[l];
+                }
+                for (uint32_t l = 0; l < m; l++) {
+                    const uint64_t want = rec[b.rec_out + g + l] & rpzstd::kOffMask;
+                    if (rpzstd::rep_at(x[l].c0, s0, s1, s2) != want) {
+                        fprintf(stderr, "case %ld: block %u sequence %u: scanned offset %u, serial %llu\n", n_cases, k,
+                                g + l, rpzstd::rep_at(x[l].c0, s0, s1, s2), (unsigned long long)want);
+                        exit(1);
+                    }
+                }
+                const rpzstd::RepFn& e = x[63];
+                const uint32_t t0 = rpzstd::rep_at(e.c0, s0, s1, s2), t1 = rpzstd::rep_at(e.c1, s0, s1, s2),
+                               t2 = rpzstd::rep_at(e.c2, s0, s1, s2);
+                s0 = t0, s1 = t1, s2 = t2;
+            }
+        }
+    }
+    bool same = v == ev && (v != 0 || len == elen);
+    Bytes out(cap + rpcodec::kSlack);
+    if (same && v == 0) {
+        n_blk_ok++;
+        rpzstd::blk_exec_serial(ip, blk, pl.nblk, lits.data(), rec.data(), out.data());
+        same = !memcmp(out.data(), eout.data(), len);
+    }
+    if (!same) {
+        fprintf(stderr, "case %ld: blocks v=%d len=%llu, decoder v=%d len=%llu, input %zu bytes, %u blocks\n", n_cases,
+                v, (unsigned long long)len, ev, (unsigned long long)elen, n, pl.nblk);
+        FILE* fp = fopen("zstd_fuzz_fail.bin", "wb");
+        if (fp) {
+            fwrite(ip, 1, n, fp);
+            fclose(fp);
+        }
+        exit(1);
+    }
+}
+
 void compare(const Bytes& in) {
     n_cases++;
     Bytes padded = in;
@@ -378,6 +453,7 @@ void compare(const Bytes& in) {
         n_ring++;
         ev = rpzstd::uncompress<true>(em, ip, in.size(), eout.data(), cap, &elen, ws);
     }
+    compare_blk(ip, in.size(), cap, ev, elen, eout);
     static Bytes oout(96u << 20);
     size_t olen = 0;
     const int32_t ov = orc_uncompress(4, ip, in.size(), oout.data(), oout.size(), &olen);
@@ -645,5 +721,6 @@ int main(int argc, char** argv) {
            n_cases, n_ring, n_ok, n_rejected);
     printf("split decoder: %ld cases == one-lane decoder, %ld handed back, %ld not planned\n", n_split, n_split_fb,
            n_split_no);
+    printf("block-parallel path: %ld large frames planned, %ld decoded: == decoder\n", n_blk, n_blk_ok);
     return 0;
 }

@@ -565,3 +565,64 @@ def test_zstd_split_decoder(case, mode):
     assert ((v == abi.V_OK) & (codec == 4)).sum() > n // 4
     if case == "mutated":
         assert ((v != abi.V_OK) & (codec == 4)).sum() > 20
+
+
+def large_mutated_zstd(rng, n):
+    """Multi-block zstd frames (200 KiB - 1 MiB of records) mutated as
+    mutated_bodies does: flipped bytes, truncation, junk, a second frame, 0xFF."""
+    out = []
+    for i in range(n):
+        recs = records(rng, int(rng.integers(180, 900)), 8, 1100, text=bool(i % 3))
+        comp = bytearray(orc.compress(4, b"".join(recs)))
+        kind = i % 6
+        if kind == 1:
+            for _ in range(int(rng.integers(1, 4))):
+                comp[int(rng.integers(0, len(comp)))] ^= int(rng.integers(1, 256))
+        elif kind == 2:
+            comp = comp[:int(rng.integers(len(comp) // 2, len(comp) + 1))]
+        elif kind == 3:
+            comp += bytes(rng.integers(0, 256, int(rng.integers(1, 9)), dtype=np.uint8))
+        elif kind == 4:
+            comp[int(rng.integers(16, len(comp)))] = 0xFF
+        out.append((bytes(comp), len(recs)))
+    return out
+
+
+@pytest.mark.parametrize("case", ["large", "mutated"])
+def test_zstd_block_parallel(case):
+    """Large zstd frames decoded block-parallel (rpgpu_zblk.h: the blocks'
+    literals and sequences by separate lanes, repeat offsets resolved by a wave
+    scan, one wave executing each frame) against the oracle, and byte for byte
+    against the one-wave decoder (RPGPU_OPT_ZSTD_WAVE_ONLY) on the same arena:
+    verdicts, lengths, rewritten batches, index.  Cases: C5-shaped bodies of
+    200 KiB - 1 MiB with 1 % corrupted batches, and library frames of 2-8
+    blocks mutated (errors found by any stage in any block).  The plan's
+    output holds the block decoder's literal and record regions."""
+    from redpanda_amd import abi, engine
+
+    if case == "large":
+        spec = engine.make_spec(seed=0x5EED0B01, partitions=64, codec_mix=1 << 4, body_min=200_000,
+                                body_max=1 << 20, ops=abi.OPS_PRODUCE | abi.OP_DECOMP, payload=abi.PAYLOAD_TEXT,
+                                corrupt_ppm=10_000, corrupt_mask=0x3FF)
+        data, descs = engine.build_arena(spec, 400)
+    else:
+        rng = np.random.default_rng(0xB02)
+        bs = [batch(c, fmt=WIRE, record_count=rc, attrs=4) for c, rc in large_mutated_zstd(rng, 120)]
+        data, descs = arena(bs, fmt=WIRE, ops=OPS)
+    with engine.Engine(0) as e:
+        got = e.decompress_arena(data, descs)
+    with engine.Engine(0, zstd_blocks=False) as e:
+        one = e.decompress_arena(data, descs)
+    for f in ("dres", "out_descs", "out_results"):
+        assert np.array_equal(got[f].view(np.uint8), one[f].view(np.uint8)), f
+    ok = np.nonzero(got["dres"]["verdict"] == abi.V_OK)[0]
+    for i in ok:
+        a = int(got["dres"]["out_offset"][i])
+        m = 61 + int(got["dres"]["out_len"][i])
+        assert np.array_equal(got["out"][a:a + m], one["out"][a:a + m]), f"batch {i}"
+    want = compare(got, data, descs, nthreads=8)
+    assert got["out_bytes"] > one["out_bytes"], "no frame took the block-parallel path"
+    v = want["verdicts"]
+    assert (v == abi.V_OK).sum() > (len(v) // 2 if case == "mutated" else len(v) * 9 // 10)
+    if case == "mutated":
+        assert (v == abi.V_DECOMP_ERROR).sum() > 10
