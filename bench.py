@@ -113,32 +113,41 @@ def effective_cores() -> tuple[int, dict]:
     return max(1, t), {"affinity_cpus": aff, "cgroup_cpu_quota": quota, "machine_cpus": os.cpu_count()}
 
 
-def quiet_cpus(t: int, window: float = 0.3) -> list[int]:
+def cpu_ticks() -> dict:
+    """Per CPU (busy, total) jiffies from /proc/stat."""
+    out = {}
+    try:
+        for line in open("/proc/stat"):
+            if line.startswith("cpu") and line[3].isdigit():
+                f = line.split()
+                v = list(map(int, f[1:]))
+                out[int(f[0][3:])] = (sum(v) - v[3] - (v[4] if len(v) > 4 else 0), sum(v))
+    except OSError:
+        pass
+    return out
+
+
+def busy_frac(a: dict, b: dict, c: int) -> float:
+    if c not in a or c not in b or b[c][1] == a[c][1]:
+        return 0.0
+    return (b[c][0] - a[c][0]) / (b[c][1] - a[c][1])
+
+
+def quiet_cpus(t: int, window: float = 0.3, busy_out: dict | None = None) -> list[int]:
     """t CPUs of this job's affinity set on distinct physical cores, the least
     busy over a short /proc/stat window first (the box is shared: CPUs another
-    job keeps busy would time that job, not the baseline)."""
+    job keeps busy would time that job, not the baseline).  busy_out, if given,
+    receives every affinity CPU's busy fraction over that window."""
     aff = sorted(os.sched_getaffinity(0))
-
-    def ticks():
-        out = {}
-        try:
-            for line in open("/proc/stat"):
-                if line.startswith("cpu") and line[3].isdigit():
-                    f = line.split()
-                    v = list(map(int, f[1:]))
-                    out[int(f[0][3:])] = (sum(v) - v[3] - (v[4] if len(v) > 4 else 0), sum(v))
-        except OSError:
-            pass
-        return out
-
-    a = ticks()
+    a = cpu_ticks()
     time.sleep(window)
-    b = ticks()
+    b = cpu_ticks()
 
     def busy(c):
-        if c not in a or c not in b or b[c][1] == a[c][1]:
-            return 0.0
-        return (b[c][0] - a[c][0]) / (b[c][1] - a[c][1])
+        return busy_frac(a, b, c)
+
+    if busy_out is not None:
+        busy_out.update({c: busy(c) for c in aff})
 
     def core(c):
         try:
@@ -653,8 +662,11 @@ def main() -> int:
 
         # one pinned worker thread per core of the job's CPU set (unpinned
         # threads gave run-to-run spreads of 1.6x); min / median / max of the runs
-        pin = quiet_cpus(T)
+        pre_busy: dict = {}
+        pin = quiet_cpus(T, busy_out=pre_busy)
         orc.set_pin(pin)
+        load_before = os.getloadavg()[0] if hasattr(os, "getloadavg") else None
+        ticks_before = cpu_ticks()
 
         def timed(th):
             cpu_pass(th)  # warm-up
@@ -668,6 +680,19 @@ def main() -> int:
 
         cpu1, spread1 = timed(1)
         cpuT, spreadT = timed(T) if T > 1 else (cpu1, spread1)
+        # how busy the host was -- the pinned CPUs just before
+        # timing, the job's other CPUs while it ran (other jobs' load there shares
+        # memory bandwidth and caches with the baseline), the 1-minute load average
+        ticks_after = cpu_ticks()
+        others = [c for c in sorted(os.sched_getaffinity(0)) if c not in pin]
+        host_busy = {
+            "pinned_cpus_busy_before": [round(pre_busy.get(c, 0.0), 3) for c in pin],
+            "other_cpus_busy_during_mean": (round(float(np.mean([busy_frac(ticks_before, ticks_after, c)
+                                                                  for c in others])), 3) if others else None),
+            "other_cpus": len(others),
+            "loadavg_1m_before": round(load_before, 2) if load_before is not None else None,
+            "loadavg_1m_after": round(os.getloadavg()[0], 2) if hasattr(os, "getloadavg") else None,
+        }
         want = cpu_pass(T)
         # the GPU's timed output for the same batches must equal the oracle's
         names = [f for f in abi.RESULT_DTYPE.names if f != "index_first"]
@@ -700,7 +725,7 @@ def main() -> int:
             "value": round(cpuT, 3), "unit": "GB/s", "cores": T, "kind": "port",
             "single_thread_gbps": round(cpu1, 3), "min_median_max_gbps": spreadT,
             "single_thread_min_median_max_gbps": spread1, "pinned_cpus": pin,
-            "cpu_model": cpu_model(), **hostinfo,
+            "cpu_model": cpu_model(), **hostinfo, "host_busy": host_busy,
             "sample": f"first {sample_n} batches of this workload ({sw / 1e9:.3f} GB wire), median of "
                       f"{args.cpu_runs} runs after a warm-up, at 1 and {T} threads (partitions round-robin "
                       f"over threads, one thread per Seastar shard, each pinned to its own physical core: the least busy of the job's CPU set): oracle/ C restatement (SSE4.2 "

@@ -229,8 +229,10 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
     if (opts && opts->walk_chunks >= 1 && opts->walk_chunks <= rpgpu::kMaxRunChunks) c->overlap.chunks = opts->walk_chunks;
     c->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     c->have_dstreams = hipStreamCreateWithFlags(&c->dstreams.aux, hipStreamNonBlocking) == hipSuccess &&
+                       hipStreamCreateWithFlags(&c->dstreams.aux2, hipStreamNonBlocking) == hipSuccess &&
                        hipEventCreateWithFlags(&c->dstreams.fork, hipEventDisableTiming) == hipSuccess &&
                        hipEventCreateWithFlags(&c->dstreams.join, hipEventDisableTiming) == hipSuccess &&
+                       hipEventCreateWithFlags(&c->dstreams.join2, hipEventDisableTiming) == hipSuccess &&
                        hipEventCreateWithFlags(&c->dstreams.parts, hipEventDisableTiming) == hipSuccess;
     c->have_overlap = hipStreamCreateWithFlags(&c->overlap.aux, hipStreamNonBlocking) == hipSuccess;
     for (int k = 0; c->have_overlap && k <= c->overlap.chunks; k++)
@@ -281,8 +283,13 @@ void rpgpu_close(rpgpu_ctx* c) {
         (void)hipStreamSynchronize(c->dstreams.aux);
         (void)hipStreamDestroy(c->dstreams.aux);
     }
+    if (c->dstreams.aux2) {
+        (void)hipStreamSynchronize(c->dstreams.aux2);
+        (void)hipStreamDestroy(c->dstreams.aux2);
+    }
     if (c->dstreams.fork) (void)hipEventDestroy(c->dstreams.fork);
     if (c->dstreams.join) (void)hipEventDestroy(c->dstreams.join);
+    if (c->dstreams.join2) (void)hipEventDestroy(c->dstreams.join2);
     if (c->dstreams.parts) (void)hipEventDestroy(c->dstreams.parts);
     delete c;
 }

@@ -218,11 +218,26 @@ size_t decomp_scratch_bytes(uint32_t n, uint32_t ws_cap) { return zblk_offset(n,
 // slots above this go to the wave decoders (a lane's serial decode of a
 // large body would hold up the whole launch)
 constexpr uint64_t kLaneMaxSlot = 256u << 10;
+#ifndef RPGPU_ZSTD_LANE_STREAM
+#define RPGPU_ZSTD_LANE_STREAM 1
+#endif
 #ifndef RPGPU_ZSTD_LANE_MAX
 #define RPGPU_ZSTD_LANE_MAX (256u << 10)
 #endif
 constexpr uint64_t kZstdLaneMaxSlot = RPGPU_ZSTD_LANE_MAX;  // zstd: its lane / wave boundary
 __device__ __forceinline__ uint64_t lane_max(uint32_t codec) { return codec == 4 ? kZstdLaneMaxSlot : kLaneMaxSlot; }
+// zstd frames above this content size leave the lane decoder even in a lane-sized slot
+#ifndef RPGPU_ZSTD_BLK_MIN
+#define RPGPU_ZSTD_BLK_MIN (80u << 10)
+#endif
+constexpr uint64_t kZstdBlkMin = RPGPU_ZSTD_BLK_MIN;
+// the first frame's content size, 0 when it has none (or the body is no frame)
+__device__ __forceinline__ uint64_t zstd_content_size(const uint8_t* b, uint64_t n) {
+    if (n < 5 || rpcodec::le32(b) != rpzstd::kMagic) return 0;
+    rpzstd::Frame h;
+    if (rpzstd::frame_header(b, n, h) != 0 || h.fcs == rpzstd::kUnknown) return 0;
+    return h.fcs;
+}
 // LZ4 / snappy-java slots above this are split into parts when the frame allows
 // (at most kLaneMaxSlot: the lane decoders take the unsplit ones below it).
 // 80 KiB: a 64 KiB block (C3) stays one lane's; bigger frames no longer leave a
@@ -285,7 +300,7 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
     __shared__ uint32_t pbase[2];
     const uint32_t i = blockIdx.x * kScanBlock + threadIdx.x;
     uint64_t sz = 0, need = 0;
-    bool over = false, wanted = false;
+    bool over = false, wanted = false, zwave = false;
     uint32_t codec = 0, np = 0;
     const uint8_t* b = nullptr;
     uint64_t body = 0;
@@ -311,6 +326,12 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
         // large batches: LZ4 frames / snappy-java bodies with a split plan go
         // to the part decoders (LZ4 parts at parts[0..), snappy's at
         // parts[pcap / 2..)); the rest to the wave decoders
+        // zstd: slots above the lane size, and frames of a known content size above
+        // kZstdBlkMin (their slot is at least blockSizeMax, so size alone does not tell
+        // them from C4's 66 KB frames) go to the wave list -- the block-parallel
+        // decoder takes what it can plan, the wave decoder the rest
+        if (wanted && !over && codec == 4)
+            zwave = sz > lane_max(4) || zstd_content_size(b, body) > kZstdBlkMin;
         if (wanted && !over && (codec == 2 || codec == 3) && sz > kSplitMinSlot) {
             auto none = [](uint32_t, uint32_t, uint64_t, uint64_t, uint64_t, uint64_t, uint32_t) {};
             np = codec == 3 ? rpcodec::lz4f_split(b, body, half, none) : rpcodec::snappy_java_split(b, body, half, none);
@@ -383,16 +404,15 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
                 }
             }
         }
-        if (wanted && !over && !sc && sz > lane_max(codec)) {
-            if (codec == 4) wlist[atomicAdd(wcount, 1u)] = i;
-            else if (codec == 2 || codec == 3) wlist[n + atomicAdd(wcount + 1, 1u)] = i;
-        }
+        if (codec == 4 && zwave) wlist[atomicAdd(wcount, 1u)] = i;
+        else if (wanted && !over && !sc && sz > lane_max(codec) && (codec == 2 || codec == 3))
+            wlist[n + atomicAdd(wcount + 1, 1u)] = i;
         sfirst[i] = sf;
         scount[i] = sc;
     }
     // zstd batches for the lane decoder (not wave-owned; overflowing ones too,
     // for their verdict): listed with one atomic per wave
-    const bool zl = i < n && wanted && codec == 4 && (over || sz <= lane_max(4));
+    const bool zl = i < n && wanted && codec == 4 && !zwave;
     const uint64_t zm = __ballot(zl);
     if (zm) {
         uint32_t zb = 0;
@@ -893,7 +913,7 @@ __global__ __launch_bounds__(256) void zblk_plan_kernel(
     const rpgpu_batch_desc d = descs[i];
     const rpgpu_batch_result v = vres[i];
     const uint64_t sz = slot[i];
-    if (enabled && decomp_wanted(d, v) && v.codec == 4 && !(sz & kOverCeiling) && sz > lane_max(4)) {
+    if (enabled && decomp_wanted(d, v) && v.codec == 4 && !(sz & kOverCeiling) && sz != 0) {
         const uint8_t* in = data + d.offset + kHeaderSize;
         const uint64_t cap = sz - kHeaderSize - rpcodec::kSlack;
         const rpzstd::BlkPlan pl = rpzstd::plan_blocks(in, body_len(v), cap, nullptr);
@@ -916,8 +936,8 @@ __global__ __launch_bounds__(256) void zblk_plan_kernel(
     frames[k] = f;
 }
 
-// E1 + E2: one lane per task (block b's literals: task 2b, its sequences:
-// task 2b + 1), each lane's Huffman / FSE workspace in LDS
+// E1 + E2: one lane per task (block b's sequences: task b, its literals: task
+// used + b), each lane's Huffman / FSE workspace in LDS
 union ZbWs {
     rpzstd::HufWs h;
     rpzstd::SeqWs s;
@@ -933,13 +953,19 @@ __global__ __launch_bounds__(64) void zblk_entropy_kernel(
     const uint32_t used = counter[28] < kBlkPool ? counter[28] : kBlkPool;
     const uint64_t loff = cnt64(counter, 30), roff = cnt64(counter, 32);
     const uint32_t lanes = gridDim.x * per_wg;
+    // tasks [0, used): the blocks' sequences (the longer ones), then [used, 2 used) their
+    // literals -- a lane's tasks alternate between the kinds whatever the grid's parity
     for (uint32_t t = blockIdx.x * per_wg + l; t < 2 * used; t += lanes) {
-        const uint32_t b = t >> 1, k = bframe[b];
+        const bool seq = t < used;
+        const uint32_t b = seq ? t : t - used, k = bframe[b];
         if (k == ~0u) continue;
+#ifdef RPZB_DIAG_TASKS  // diagnostics build: 1 literals only, 2 sequences only (timing)
+        if ((seq ? 2 : 1) != RPZB_DIAG_TASKS) continue;
+#endif
         const ZbFrame f = frames[k];
         const uint8_t* in = data + descs[wlist[k]].offset + kHeaderSize;
         const uint32_t j = b - f.first;
-        if (t & 1)
+        if (seq)
             pool[b].e2 = rpzstd::blk_sequences(in, pool + f.first, j, reinterpret_cast<uint64_t*>(out + roff) + f.recs, w.s);
         else
             pool[b].e1 = rpzstd::blk_literals(in, pool + f.first, j, out + loff + f.lits, w.h);
@@ -1369,13 +1395,74 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     decomp_counters_kernel<<<1, 64, 0, s>>>(p.counter, 1);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    // large batches on the wave decoders, on a second stream beside the lanes
-    hipStream_t ws = s;
+    // large batches on the wave decoders, on a second stream beside the lanes;
+    // the zstd / gzip lane decoders on a third (RPGPU_ZSTD_LANE_STREAM 0: on the
+    // main stream after the LZ4 / snappy lanes, as before round 5)
+    hipStream_t ws = s, zs = s;
     if (ds) {
         if ((e = hipEventRecord(ds->fork, s)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(ds->aux, ds->fork, 0)) != hipSuccess) return e;
         ws = ds->aux;
+#if RPGPU_ZSTD_LANE_STREAM
+        if ((e = hipStreamWaitEvent(ds->aux2, ds->fork, 0)) != hipSuccess) return e;
+        zs = ds->aux2;
+#endif
     }
+    // the zstd / gzip lane decoders (on zs)
+    auto zlanes = [&]() -> hipError_t {
+        hipError_t e = hipSuccess;
+        const uint32_t zl = zstd_lanes(n, ws_cap);  // the HBM-workspace lane decoder (at most zl lanes)
+        // the split decoder over the zstd lane batches it planned: A1 literals, A2
+        // decisions + records, B execution; what A2 hands back, the one-lane decoder
+        const ZParts z = zparts(d_scratch, n, ws_cap);
+        if ((zmode & 3) == 2) {
+            zseq_fused_kernel<<<(zl + 255) / 256, 256, 0, zs>>>(
+                d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.counter,
+                p.wlist + 2 * (size_t)n, z.flag, z.lits, z.bs_l, z.szl, z.recs, z.bs_r, z.szr);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            zseq_exec_kernel<<<(zl + 255) / 256, 256, 0, zs>>>(p.counter, p.wlist + 2 * (size_t)n, z.flag, z.recs, z.bs_r,
+                                                             p.local, p.block_sum, d_out);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        } else if ((zmode & 3) == 1) {
+    #ifdef RPZS_HBM_WS
+            const uint32_t zl_n = n < RPZ_LANES ? n : RPZ_LANES;
+            const ZLaunch zq{(zl_n + 255) / 256, 256, 256};
+            const size_t lit_lds = 0, seq_lds = 0;
+    #else
+            const ZLaunch zq = zseq_launch();
+            const size_t lit_lds = zq.lit_lanes * sizeof(rpzstd::HufWs), seq_lds = zq.seq_lanes * sizeof(rpzstd::SeqWs);
+    #endif
+            zseq_lit_kernel<<<zq.grid, RPZS_WG, lit_lds, zs>>>(
+                d_descs, d_data, d_vres, p.counter, p.wlist + 2 * (size_t)n, z.flag, z.lits, z.bs_l, z.szl, z.sec, d_out,
+                zq.lit_lanes, z.hws);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            zseq_seq_kernel<<<zq.grid, RPZS_WG, seq_lds, zs>>>(
+                d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.counter,
+                p.wlist + 2 * (size_t)n, z.flag, z.lits, z.bs_l, z.szl, z.recs, z.bs_r, z.szr, z.sec, zq.seq_lanes, z.hws);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            zseq_exec_kernel<<<(zl + 255) / 256, 256, 0, zs>>>(p.counter, p.wlist + 2 * (size_t)n, z.flag, z.recs, z.bs_r,
+                                                             p.local, p.block_sum, d_out);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        ws_lane_kernel<4><<<(zl + 255) / 256, 256, 0, zs>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres,
+                                                             d_out, out_cap, d_out_descs, nullptr, p.counter,
+                                                             p.wlist + 2 * (size_t)n, z.flag);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        zstd_ring_kernel<<<(zl + 255) / 256, 256, 0, zs>>>(d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres,
+                                                          d_out, out_cap, d_out_descs, p.counter, p.wlist + 2 * (size_t)n);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        const uint32_t gl = gzip_lanes(n, ws_cap);
+        ws_lane_kernel<1><<<(gl + 255) / 256, 256, 0, zs>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
+                                                             d_dres, d_out, out_cap, d_out_descs, p.gws, p.counter,
+                                                             nullptr, nullptr);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        return hipSuccess;
+    };
+#if RPGPU_ZSTD_LANE_STREAM
+    // first: their 256-VGPR waves need half a CU's registers, which the part and
+    // lane kernels' waves would otherwise hold until they drain
+    if (ds && (e = zlanes()) != hipSuccess) return e;
+#endif
     // split batches: LZ4 and snappy parts ahead of the lane kernels on the main
     // stream, then their verdicts on the second, after its zstd wave decoder
     // (failures join the LZ wave list).  With bodies split above 80 KiB the
@@ -1423,54 +1510,18 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     decomp_lane_kernel<2><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
                                               out_cap, d_out_descs, p.scount);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const uint32_t zl = zstd_lanes(n, ws_cap);  // the HBM-workspace lane decoder (at most zl lanes)
-    // the split decoder over the zstd lane batches it planned: A1 literals, A2
-    // decisions + records, B execution; what A2 hands back, the one-lane decoder
-    const ZParts z = zparts(d_scratch, n, ws_cap);
-    if ((zmode & 3) == 2) {
-        zseq_fused_kernel<<<(zl + 255) / 256, 256, 0, s>>>(
-            d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.counter,
-            p.wlist + 2 * (size_t)n, z.flag, z.lits, z.bs_l, z.szl, z.recs, z.bs_r, z.szr);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        zseq_exec_kernel<<<(zl + 255) / 256, 256, 0, s>>>(p.counter, p.wlist + 2 * (size_t)n, z.flag, z.recs, z.bs_r,
-                                                         p.local, p.block_sum, d_out);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    } else if ((zmode & 3) == 1) {
-#ifdef RPZS_HBM_WS
-        const uint32_t zl_n = n < RPZ_LANES ? n : RPZ_LANES;
-        const ZLaunch zq{(zl_n + 255) / 256, 256, 256};
-        const size_t lit_lds = 0, seq_lds = 0;
+#if !RPGPU_ZSTD_LANE_STREAM
+    if ((e = zlanes()) != hipSuccess) return e;
 #else
-        const ZLaunch zq = zseq_launch();
-        const size_t lit_lds = zq.lit_lanes * sizeof(rpzstd::HufWs), seq_lds = zq.seq_lanes * sizeof(rpzstd::SeqWs);
+    if (!ds && (e = zlanes()) != hipSuccess) return e;
 #endif
-        zseq_lit_kernel<<<zq.grid, RPZS_WG, lit_lds, s>>>(
-            d_descs, d_data, d_vres, p.counter, p.wlist + 2 * (size_t)n, z.flag, z.lits, z.bs_l, z.szl, z.sec, d_out,
-            zq.lit_lanes, z.hws);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        zseq_seq_kernel<<<zq.grid, RPZS_WG, seq_lds, s>>>(
-            d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.counter,
-            p.wlist + 2 * (size_t)n, z.flag, z.lits, z.bs_l, z.szl, z.recs, z.bs_r, z.szr, z.sec, zq.seq_lanes, z.hws);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        zseq_exec_kernel<<<(zl + 255) / 256, 256, 0, s>>>(p.counter, p.wlist + 2 * (size_t)n, z.flag, z.recs, z.bs_r,
-                                                         p.local, p.block_sum, d_out);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
-    ws_lane_kernel<4><<<(zl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres,
-                                                         d_out, out_cap, d_out_descs, nullptr, p.counter,
-                                                         p.wlist + 2 * (size_t)n, z.flag);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    zstd_ring_kernel<<<(zl + 255) / 256, 256, 0, s>>>(d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres,
-                                                      d_out, out_cap, d_out_descs, p.counter, p.wlist + 2 * (size_t)n);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    const uint32_t gl = gzip_lanes(n, ws_cap);
-    ws_lane_kernel<1><<<(gl + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
-                                                         d_dres, d_out, out_cap, d_out_descs, p.gws, p.counter,
-                                                         nullptr, nullptr);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     if (ds) {
         if ((e = hipEventRecord(ds->join, ds->aux)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(s, ds->join, 0)) != hipSuccess) return e;
+#if RPGPU_ZSTD_LANE_STREAM
+        if ((e = hipEventRecord(ds->join2, ds->aux2)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(s, ds->join2, 0)) != hipSuccess) return e;
+#endif
     }
     if ((e = launch_plan(d_out_descs, n, d_out, d_index_used, p.vscratch, s)) != hipSuccess) return e;
     // no chunked walk overlap here: the rewritten arena is walked in one launch (16

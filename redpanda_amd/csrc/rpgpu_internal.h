@@ -48,10 +48,11 @@ struct Overlap {
 };
 
 // rpgpu_decomp_run_device: the large batches' wave decoders run on `aux`
-// beside the lane decoders (fork / join events)
+// beside the LZ4 / snappy lane and part decoders, the zstd and gzip lane
+// decoders on `aux2` (fork / join events)
 struct DecompStreams {
-    hipStream_t aux;
-    hipEvent_t fork, join, parts;  // parts: the LZ4 part decoder (main stream) is done
+    hipStream_t aux, aux2;
+    hipEvent_t fork, join, join2, parts;  // parts: the LZ4 part decoder (main stream) is done
 };
 
 void build_tables(uint32_t* out /* kTableWords */);

@@ -276,6 +276,14 @@ RPC_HD bool huf_select_x2(uint64_t dst, uint64_t csrc) {
 // LDS for the wave decoder and the scalar mirror.  (A compact ~7.6 KB form
 // without the X1 table, for one workspace per lane in LDS, measured 5.5x
 // slower per C4 step in round 3 and was removed.)
+// bytes [at, at + len) of the flat output as an over-long copy left them in
+// the ring: byte k is p[k % period], or (period 0) p[k] below lim, else pad
+struct GRun {
+    const uint8_t* p;
+    uint64_t at;
+    uint32_t len, period, lim;
+    int32_t pad;
+};
 struct Ws {
     static constexpr bool kHasX = true;  // llx / mlx (filled for workspaces in LDS)
     uint16_t huf[1u << kHufMaxLog];  // X1 table: symbol | nbBits << 8
@@ -291,6 +299,12 @@ struct Ws {
     uint32_t rank[kHufMaxLog + 1];
     uint64_t rep[3];
     uint64_t ring_v, ring_p;  // the ring's previous and current segment (flat offsets)
+    uint64_t ring_e;          // the ring's end for the current segment (flat)
+    // what libzstd's over-long copies left in the ring past the write position
+    // g_at (ring_seq below): the last 4 copies' runs, gr[gh] the newest
+    GRun gr[4];
+    uint32_t gh;
+    uint64_t g_at;
     uint8_t ll_log, ml_log, of_log, huf_log;
     uint8_t huf_x2, lit_entropy, fse_entropy, huf1_on;
 #if RPZ_PROF
@@ -816,6 +830,10 @@ struct DirectEmit {
 struct Lit {
     const uint8_t* p;  // literal bytes (input, or the output slot's tail)
     uint64_t n;
+    // what libzstd's literal buffer holds past them (read by over-long copies):
+    // -1 the input itself (raw literals referenced in place), else this byte
+    // (0 after Huffman literals and raw ones copied to litBuffer, the RLE byte)
+    int32_t pad;
 };
 
 // ZSTD_decodeLiteralsBlock.  Huffman / RLE literals go to out[tail - n, tail).
@@ -842,6 +860,7 @@ RPZ_COLD int64_t literals(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* o
             if (hs + size > n) return RPZ_FAIL(-1);
             lit.p = in + hs;
             lit.n = size;
+            lit.pad = hs + size + 32 > n ? 0 : -1;  // WILDCOPY_OVERLENGTH: copied to litBuffer, else in place
             return (int64_t)(hs + size);
         }
         if (lh == 3 && n < 4) return RPZ_FAIL(-1);
@@ -852,6 +871,7 @@ RPZ_COLD int64_t literals(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* o
         em.litfill(d, v, size);
         lit.p = d;
         lit.n = size;
+        lit.pad = v;  // memset(litBuffer, v, litSize + WILDCOPY_OVERLENGTH)
         return (int64_t)(hs + 1);
     }
     // compressed (2) / repeat (3)
@@ -931,6 +951,7 @@ RPZ_COLD int64_t literals(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* o
     w.lit_entropy = 1;
     lit.p = d;
     lit.n = size;
+    lit.pad = 0;
     return (int64_t)(hs + csize);
 }
 
@@ -1017,6 +1038,140 @@ RPC_HD void ring_match(E& em, uint8_t* out, uint64_t lit_end, uint64_t offset, u
     if (ml > k1) em.match(out + lit_end + k1, offset, ml - k1);
     else em.sync();
 }
+// ---- libzstd's over-long copies in a wrapped ring (ZSTD_execSequence 1.4.9)
+// Its copies write past their end: literals ZSTD_copy16 then ZSTD_wildcopy,
+// matches ZSTD_wildcopy (offset >= 16) or ZSTD_overlapCopy8 + 8-byte steps;
+// near the ring's end (the sequence ending within WILDCOPY_OVERLENGTH of it)
+// ZSTD_execSequenceEnd's ZSTD_safecopy.  The next sequence overwrites those
+// bytes, except where a match reads the previous segment (the extDict) just
+// past the write position: it reads them.  The restatement keeps the flat
+// output and records what lies past the write position as runs of source
+// bytes (the literal buffer's continuation, or the match's own period).
+#ifdef RPZ_BAND_STATS
+inline long rpz_band_reads = 0, rpz_end_path = 0;
+#endif
+RPC_HD uint64_t wild_w(uint64_t len) {  // bytes ZSTD_wildcopy writes (16-byte steps)
+    return len <= 16 ? 16 : 16 + 32 * ((len - 16 + 31) / 32);
+}
+RPC_HD uint64_t cp8_w(uint64_t len) {  // ZSTD_overlapCopy8, then 8-byte steps
+    return len <= 8 ? 8 : 8 + 8 * ((len - 8 + 7) / 8);
+}
+// bytes ZSTD_safecopy(op, oend_w, ip, len, ovtype) writes past op + len
+RPC_HD uint64_t safe_over(uint64_t op, uint64_t len, uint64_t oend_w, bool src_before, uint64_t off) {
+    if (len < 8) return 0;
+    const uint64_t oend = op + len;
+    uint64_t o = op;
+    if (src_before) o += 8;  // ZSTD_overlapCopy8
+    const bool small = src_before && off < 16;
+    if (oend <= oend_w) {
+        const uint64_t e = o + (small ? (len - (o - op) == 0 ? 8 : 8 * ((len - (o - op) + 7) / 8)) : wild_w(len - (o - op)));
+        return e > oend ? e - oend : 0;
+    }
+    if (o <= oend_w) {
+        const uint64_t l = oend_w - o;
+        const uint64_t e = o + (small ? (l == 0 ? 8 : 8 * ((l + 7) / 8)) : wild_w(l));
+        return e > oend ? e - oend : 0;
+    }
+    return 0;
+}
+// how far past the write position g_at the runs reach
+template <class W>
+RPC_HD uint64_t g_end(const W& w) {
+    uint64_t e = 0;
+    for (uint32_t i = 0; i < 4; i++) {
+        const uint64_t x = w.gr[i].at + w.gr[i].len;
+        if (w.gr[i].len && x > w.g_at && x - w.g_at > e) e = x - w.g_at;
+    }
+    return e;
+}
+// the ring's byte at flat position x >= g_at: the newest run covering it, else `orig`
+template <class W>
+RPC_HD uint8_t g_byte(const W& w, uint64_t x, uint8_t orig) {
+    for (uint32_t n = 0; n < 4; n++) {
+        const GRun& r = w.gr[(w.gh + 4 - n) & 3];
+        if (x >= r.at && x < r.at + r.len) {
+            const uint64_t k = x - r.at;
+            return r.period ? r.p[k % r.period] : (k < r.lim ? r.p[k] : (uint8_t)r.pad);
+        }
+    }
+    return orig;
+}
+template <class W>
+RPC_HD void g_reset(W& w, uint64_t at) {
+    for (uint32_t i = 0; i < 4; i++) w.gr[i].len = 0;
+    w.gh = 0;
+    w.g_at = at;
+}
+// len bytes written exactly at `at`, then `over` more as run `nr` describes
+template <class W>
+RPC_HD void g_copy(W& w, uint64_t at, uint64_t len, uint64_t over, const GRun& nr) {
+    if (w.g_at != at) g_reset(w, at);  // (not reached: copies are contiguous)
+    w.g_at = at + len;
+    if (over) {
+        w.gh = (w.gh + 1) & 3;
+        GRun& r = w.gr[w.gh];
+        r = nr;
+        r.at = at + len;
+        r.len = (uint32_t)over;
+    }
+}
+// One sequence in a wrapped ring (vstart < pstart): copies as block() makes
+// them, with the extDict bytes past the write position taken from what the
+// over-long copies left there, and the runs updated.
+template <class E, class W>
+RPC_HD void ring_seq(E& em, W& w, uint8_t* out, uint64_t o, const uint8_t* lp, const uint8_t* lend, int32_t pad,
+                     uint64_t ll, uint64_t ml, uint64_t offset, uint64_t vstart, uint64_t pstart) {
+    const uint64_t lit_end = o + ll, oend_w = w.ring_e - 32;
+    const bool endp = lit_end + ml > oend_w;  // ZSTD_execSequenceEnd
+#ifdef RPZ_BAND_STATS
+    rpz_end_path += endp;
+#endif
+    em.lits(out + o, lp, ll);
+    {
+        const uint64_t over = endp ? safe_over(o, ll, oend_w, false, 0)
+                                   : (ll <= 16 ? 16 - ll : 16 + wild_w(ll - 16) - ll);
+        GRun r{};
+        r.p = lp + ll;
+        r.lim = pad < 0 ? 0xFFFFFFFFu : (uint32_t)(lend - (lp + ll));
+        r.pad = pad;
+        g_copy(w, o, ll, over, r);
+    }
+    uint64_t over_m = 0;
+    if (offset > lit_end - pstart) {  // from the extDict (offset <= pstart - vstart + lit_end - pstart)
+        const uint64_t a = lit_end - offset - vstart, lw = lit_end - pstart;
+        const uint64_t len1 = pstart - (lit_end - offset), l1 = ml < len1 ? ml : len1;
+        const uint64_t ge = g_end(w);  // g_at == lit_end here
+        if (a < lw + ge && a + l1 > lw) {
+            // the memmove reads bytes the over-long copies left: byte by byte
+#ifdef RPZ_BAND_STATS  // host diagnostics (tests/native/zstd_fuzz.cpp): band reads seen
+            rpz_band_reads++;
+#endif
+            em.sync();
+            for (uint64_t i = 0; i < l1; i++) {
+                const uint64_t r = a + i;
+                out[lit_end + i] = r < lw ? out[pstart + r] : (r - lw < ge ? g_byte(w, pstart + r, out[vstart + r]) : out[vstart + r]);
+            }
+            if (ml > l1) em.match(out + lit_end + l1, offset, ml - l1);
+        } else if (offset > pstart - vstart) {
+            ring_match(em, out, lit_end, offset, ml, vstart, pstart);
+        } else {
+            em.match(out + lit_end, offset, ml);
+        }
+        if (ml > l1) {
+            const uint64_t m2 = ml - l1;
+            over_m = endp ? safe_over(lit_end + l1, m2, oend_w, true, offset)
+                          : (offset >= 16 ? wild_w(m2) - m2 : cp8_w(m2) - m2);
+        }
+    } else {
+        em.match(out + lit_end, offset, ml);
+        over_m = endp ? safe_over(lit_end, ml, oend_w, true, offset) : (offset >= 16 ? wild_w(ml) - ml : cp8_w(ml) - ml);
+    }
+    GRun r{};
+    r.p = out + lit_end + ml - offset;
+    r.period = (uint32_t)offset;
+    g_copy(w, lit_end, ml, over_m, r);
+}
+
 // ZSTD_decompressBlock_internal for one compressed block: output at out[op..),
 // at most `cap` bytes; literals may use the slot tail [.., tail).  History:
 // the ring segment being written starts at pstart, the previous one (the
@@ -1137,16 +1292,17 @@ RPZ_COLD int64_t block(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out,
             if (ll > (uint64_t)(lend - lp)) return RPZ_FAIL(-1);
             const uint64_t lit_end = o + ll;
             if (offset > lit_end - vstart) return RPZ_FAIL(-1);
+            if constexpr (kRing) {
+                if (vstart < pstart) {
+                    ring_seq(em, w, out, o, lp, lend, lit.pad, ll, ml, offset, vstart, pstart);
+                    lp += ll;
+                    o = lit_end + ml;
+                    continue;
+                }
+            }
             em.lits(out + o, lp, ll);
             lp += ll;
-            if constexpr (kRing) {
-                if (offset > lit_end - pstart && offset > pstart - vstart)
-                    ring_match(em, out, lit_end, offset, ml, vstart, pstart);
-                else
-                    em.match(out + lit_end, offset, ml);
-            } else {
-                em.match(out + lit_end, offset, ml);
-            }
+            em.match(out + lit_end, offset, ml);
             o = lit_end + ml;
         }
 #if RPZ_PROF
@@ -1160,7 +1316,10 @@ RPZ_COLD int64_t block(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out,
     }
     const uint64_t last = (uint64_t)(lend - lp);
     if (last > oend - o) return RPZ_FAIL(-1);
-    em.lits(out + o, lp, last);
+    em.lits(out + o, lp, last);  // ZSTD_memcpy: exact
+    if constexpr (kRing) {
+        if (vstart < pstart) g_copy(w, o, last, 0, w.gr[0]);
+    }
     o += last;
     return (int64_t)(o - op);
 }
@@ -1422,6 +1581,10 @@ RPC_HD int32_t uncompress_impl(E& em, const uint8_t* in, uint64_t n, uint8_t* ou
         }
         uint64_t decoded = 0, ostart = 0;
         w.ring_v = w.ring_p = fstart;
+        if constexpr (kRing) {
+            w.ring_e = fstart + bufs.out;
+            g_reset(w, fstart);
+        }
         bool done = false;
         for (;;) {
             if (rem - ip < 3) break;  // partial block header
@@ -1443,6 +1606,7 @@ RPC_HD int32_t uncompress_impl(E& em, const uint8_t* in, uint64_t n, uint8_t* ou
                     if (take > room_ring) return RPZ_FAIL(V_ERROR);
                     if (T + take > cap) return V_OVERFLOW;
                     em.lits(out + T, f + ip, take);
+                    if constexpr (kRing) g_copy(w, T, take, 0, w.gr[0]);  // ZSTD_copyRawBlock: exact
                     ip += take;
                     T += take;
                     decoded += take;
@@ -1455,6 +1619,7 @@ RPC_HD int32_t uncompress_impl(E& em, const uint8_t* in, uint64_t n, uint8_t* ou
                     if (size > h.bsm) return RPZ_FAIL(V_ERROR);
                     if (T + size > cap) return V_OVERFLOW;
                     em.fill(out + T, f[ip], size);
+                    if constexpr (kRing) g_copy(w, T, size, 0, w.gr[0]);  // ZSTD_setRleBlock: exact
                     ip += 1;
                     r = size;
                     T += r;
@@ -1509,6 +1674,10 @@ RPC_HD int32_t uncompress_impl(E& em, const uint8_t* in, uint64_t n, uint8_t* ou
                 ostart = 0;
                 w.ring_v = w.ring_p;
                 w.ring_p = T;
+                if constexpr (kRing) {
+                    w.ring_e = T + bufs.out;
+                    g_reset(w, T);  // the previous segment's leftovers lie past the extDict
+                }
             }
         }
         if (!done) {  // input ended inside the frame: what was decoded stands

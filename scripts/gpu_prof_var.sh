@@ -9,7 +9,7 @@ for r in $RUNS; do
   ev=""
   [ "$lib" != base ] && ev="RPGPU_DIAG_LIB=$PWD/build/vx/librpgpu_$lib.so"
   [ "$envs" != - ] && ev="$ev ${envs//,/ }"
-  env $ev timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pv_$tag -o run -- python bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/pv_$tag.json 2> gpurun_out/pv_$tag.err || { tail -5 gpurun_out/pv_$tag.err; exit 1; }
+  env $ev timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pv_$tag -o run -- python bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline $BENCH_ARGS > gpurun_out/pv_$tag.json 2> gpurun_out/pv_$tag.err || { tail -5 gpurun_out/pv_$tag.err; exit 1; }
   f=$(find gpurun_out/pv_$tag -name "*kernel_stats.csv" | head -1)
   cp "$f" gpurun_out/pv_${tag}_kernel_stats.csv
   echo "== $tag"

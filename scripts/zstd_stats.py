@@ -8,7 +8,7 @@ block types, literals types and sizes, Huffman weight counts / header kinds,
 sequence counts and the LL / OF / ML table modes (0 predefined, 1 RLE, 2 FSE,
 3 repeat) with the FSE accuracy logs.  Pure parsing of the format, no decode.
 
-  python scripts/zstd_stats.py [--config c4] [--n 2048]
+  python scripts/zstd_stats.py [--config c4] [--n 2048] [--min-bytes 0]
 """
 import argparse
 import collections
@@ -60,6 +60,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c4")
     ap.add_argument("--n", type=int, default=2048)
+    ap.add_argument("--min-bytes", type=int, default=0, help="only bodies of at least this many compressed bytes")
     args = ap.parse_args()
     import bench
     from redpanda_amd import abi, engine
@@ -78,6 +79,8 @@ def main():
         if (int.from_bytes(bytes(b[21:23]), "big") & 7) != 4:
             continue
         body = bytes(b[61:])
+        if len(body) < args.min_bytes:
+            continue
         sums["batches"] += 1
         sums["compressed"] += len(body)
         for t, pl, fh in frame_blocks(body):

@@ -2,8 +2,12 @@
 1 KiB window makes the reference loop's ring buffer wrap every two blocks,
 each with one match whose offset reaches into the previous ring segment
 (where the current one has or has not overwritten it) or before it
-(corruption_detected in libzstd).  Made by tests/native/zstd_fuzz.cpp
---dump-ring (the engine's own zstd encoder pieces, predefined FSE tables);
+(corruption_detected in libzstd); and (`band_*`) frames whose matches, once
+the ring has wrapped, read the previous segment right past the write
+position, where libzstd's over-long copies (ZSTD_wildcopy, ZSTD_overlapCopy8,
+ZSTD_safecopy near the ring's end) left bytes -- 40 small ones (lane decoder)
+and 4 of 400 blocks (wave decoder).  Made by tests/native/zstd_fuzz.cpp
+--dump-ring / --dump-band (the engine's own zstd encoder pieces, predefined FSE tables);
 the expected outputs come from the oracle (libzstd 1.4.9 through
 stream_zstd::do_uncompress) at test time.  Writes tests/golden/zstd_ring.npz."""
 import subprocess
@@ -32,10 +36,19 @@ def main():
         for off, nb, bad in CASES:
             subprocess.run([str(exe), "--seed", "11", "--dump-ring", f"{off},{nb},{bad}"], cwd=tmp, check=True)
             frames.append(np.frombuffer((Path(tmp) / "ring.zst").read_bytes(), dtype=np.uint8))
+        subprocess.run([str(exe), "--seed", "12", "--dump-band", "40,4"], cwd=tmp, check=True)
+        raw = (Path(tmp) / "band.bin").read_bytes()
+        band, p = [], 0
+        while p < len(raw):
+            n = int.from_bytes(raw[p:p + 4], "little")
+            band.append(np.frombuffer(raw[p + 4:p + 4 + n], dtype=np.uint8))
+            p += 4 + n
     lens = np.array([len(f) for f in frames], dtype=np.int64)
+    blens = np.array([len(f) for f in band], dtype=np.int64)
     np.savez_compressed(ROOT / "tests" / "golden" / "zstd_ring.npz", data=np.concatenate(frames), lens=lens,
-                        cases=np.array(CASES, dtype=np.int64))
-    print("wrote", len(frames), "frames,", int(lens.sum()), "bytes")
+                        cases=np.array(CASES, dtype=np.int64), band_data=np.concatenate(band), band_lens=blens)
+    print("wrote", len(frames), "ring frames,", int(lens.sum()), "bytes;", len(band), "band frames,", int(blens.sum()),
+          "bytes")
 
 
 if __name__ == "__main__":

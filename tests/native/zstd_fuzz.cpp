@@ -625,17 +625,125 @@ Bytes crafted_ring_frame(int nblocks, int bad, uint32_t off) {
     return f;
 }
 
-// Not restated: libzstd's wildcopy over-writes (literal and match copies
-// write up to 32-48 bytes past their end, into the ring) -- an offset that
-// reads the extDict within 64 bytes past the current write position reads
-// those bytes.  Such offsets lie beyond the window; matches reading any
-// extDict byte there are skipped here.
-bool in_overrun_band(int bad, uint32_t off) {
-    const uint64_t lit_end = (uint64_t)bad * 1024 + 80, pstart = (uint64_t)(bad / 2) * 2048;
-    if (bad < 2 || off <= lit_end - pstart || off > lit_end - (pstart - 2048)) return false;
-    const uint64_t a = lit_end - off - (pstart - 2048), lw = lit_end - pstart;
-    const uint64_t len1 = pstart - (lit_end - off), n = len1 < 40 ? len1 : 40;  // extDict bytes read
-    return a < lw + 64 && a + n > lw;
+
+// libzstd's over-long copies (ZSTD_copy16 / ZSTD_wildcopy / ZSTD_overlapCopy8 /
+// ZSTD_safecopy near the ring's end) leave bytes past each sequence in the
+// ring; a match reading the previous segment just past the write position
+// reads them (rpgpu_zstd.h ring_seq).  Frames with a 1 KiB window (ring 2112
+// bytes, segments of up to 2112) whose sequences, once the ring has wrapped,
+// aim matches at ring positions around the write position: literal runs of
+// 0-100 bytes (raw literals read in place or copied to litBuffer), matches of
+// 3-80 bytes with short (< 16) and long offsets, blocks of 16-1024 bytes so
+// that segments end anywhere up to the ring's end (ZSTD_execSequenceEnd),
+// raw and RLE blocks between them.
+Bytes band_frame(int nblocks = 0) {
+    Bytes f = {0x28, 0xB5, 0x2F, 0xFD, 0x00, 0x00};  // no FCS / checksum; window 1 KiB
+    const uint64_t ring = 1024 + 1024 + 64, bsm = 1024;
+    uint64_t T = 0, ostart = 0, pstart = 0, vstart = 0;
+    if (nblocks <= 0) nblocks = 3 + (int)below(9);
+    const bool to_end = below(2) == 0;  // segments of 32-64 + 1024 + 1024 bytes: up to the ring's end
+    for (int k = 0; k < nblocks; k++) {
+        const uint32_t last = k + 1 == nblocks ? 1u : 0u;
+        // full blocks, and small ones that let a segment run up to the ring's end
+        const uint64_t pick = below(4);
+        const uint64_t size = to_end ? (k % 3 == 0 ? 32 + below(33) : bsm)
+                                     : (pick < 2 ? bsm : (pick == 2 ? 32 + below(33) : 16 + below(bsm - 15)));
+        const uint32_t kind = (uint32_t)below(10);
+        if (kind == 0 || kind == 1) {  // raw / RLE block
+            const uint32_t bh = last | (kind << 1) | ((uint32_t)size << 3);
+            f.push_back((uint8_t)bh), f.push_back((uint8_t)(bh >> 8)), f.push_back((uint8_t)(bh >> 16));
+            if (kind == 0)
+                for (uint64_t j = 0; j < size; j++) f.push_back((uint8_t)('a' + below(26)));
+            else
+                f.push_back((uint8_t)('A' + below(26)));
+        } else {
+            Bytes lits;
+            std::vector<rpzstdc::Seq> seqs;
+            uint64_t pos = T, produced = 0;
+            while (produced < size && seqs.size() < 100) {
+                const uint64_t rem = size - produced;
+                if (rem < 8 || below(8) == 0) break;
+                uint64_t ll = below((rem - 3 < 100 ? rem - 3 : 100) + 1);
+                const uint64_t mmax = rem - ll < 80 ? rem - ll : 80;
+                if (mmax < 3) break;
+                uint64_t ml = 3 + below(mmax - 2);
+                if (rem <= 120 && below(2) == 0) {  // end the block's sequences within 8 bytes of its end
+                    ll = below((rem - 3 < 60 ? rem - 3 : 60) + 1);
+                    const uint64_t room = rem - ll;  // >= 3
+                    ml = room - below((room - 3 < 8 ? room - 3 : 8) + 1);
+                }
+                const uint64_t lit_end = pos + ll;
+                uint64_t off;
+                if (vstart < pstart && below(3) != 0) {
+                    const uint64_t lw = lit_end - pstart, ext = pstart - vstart;
+                    int64_t r0 = (int64_t)lw + (int64_t)below(110) - 40;
+                    if (r0 < 0) r0 = 0;
+                    if ((uint64_t)r0 >= ext) r0 = (int64_t)ext - 1;
+                    off = lit_end - (vstart + (uint64_t)r0);
+                } else if (below(3) == 0) {
+                    off = 1 + below(15);
+                } else {
+                    const uint64_t lim = lit_end - vstart < 1500 ? lit_end - vstart : 1500;
+                    off = 1 + below(lim);
+                }
+                if (off > lit_end - vstart || off == 0) off = 1;
+                if (off > lit_end - vstart) break;
+                for (uint64_t j = 0; j < ll; j++) lits.push_back((uint8_t)('a' + below(26)));
+                seqs.push_back(rpzstdc::Seq{(uint32_t)ll, (uint32_t)ml, (uint32_t)off});
+                pos = lit_end + ml;
+                produced += ll + ml;
+            }
+            if (seqs.empty()) {
+                lits.push_back('x');
+                seqs.push_back(rpzstdc::Seq{1, 3, 1});
+                produced = 4;
+                if (pos - vstart < 1) break;
+            }
+            const uint64_t lastlits = size > produced ? size - produced : 0;
+            for (uint64_t j = 0; j < lastlits; j++) lits.push_back((uint8_t)('a' + below(26)));
+            produced += lastlits;
+            const Bytes blk = seq_block(lits, seqs);
+            if (blk.size() <= bsm) {
+                const uint32_t bh = last | (2u << 1) | ((uint32_t)blk.size() << 3);
+                f.push_back((uint8_t)bh), f.push_back((uint8_t)(bh >> 8)), f.push_back((uint8_t)(bh >> 16));
+                f.insert(f.end(), blk.begin(), blk.end());
+            } else {  // above blockSizeMax compressed: the same output as a raw block
+                const uint32_t bh = last | ((uint32_t)size << 3);
+                f.push_back((uint8_t)bh), f.push_back((uint8_t)(bh >> 8)), f.push_back((uint8_t)(bh >> 16));
+                for (uint64_t j = 0; j < size; j++) f.push_back((uint8_t)('a' + below(26)));
+            }
+            (void)produced;
+        }
+        // the decoder's ring: the block's output, then a wrap when the next
+        // block might not fit (uncompress_impl)
+        const uint64_t out_size = kind <= 1 ? size : size;  // every block decodes to `size`
+        T += out_size;
+        ostart += out_size;
+        if (ostart + bsm > ring) {
+            ostart = 0;
+            vstart = pstart;
+            pstart = T;
+        }
+    }
+    return f;
+}
+
+void check_band(long cases) {
+    const long ok0 = n_ok, rej0 = n_rejected;
+    for (long i = 0; i < cases; i++) {
+        Bytes f = band_frame();
+        compare(f);
+        if (below(2) && f.size() > 16) {  // and a byte flipped anywhere past the frame header
+            f[8 + below(f.size() - 8)] ^= (uint8_t)(1u << below(8));
+            compare(f);
+        }
+    }
+#ifdef RPZ_BAND_STATS
+    printf("band frames: %ld decoded, %ld rejected; band reads %ld, sequences near the ring end %ld\n", n_ok - ok0,
+           n_rejected - rej0, rpzstd::rpz_band_reads, rpzstd::rpz_end_path);
+#else
+    (void)ok0, (void)rej0;
+#endif
 }
 
 void check_ring_crafted() {
@@ -646,7 +754,6 @@ void check_ring_crafted() {
     for (int i = 0; i < 300; i++) {
         const int bad = 2 + (int)below(9);
         const uint32_t off = 1 + (uint32_t)below(1024u * (uint32_t)(bad + 1));
-        if (in_overrun_band(bad, off)) continue;
         compare(crafted_ring_frame(bad + 1 + (int)below(3), bad, off));
     }
 }
@@ -679,6 +786,20 @@ int main(int argc, char** argv) {
         if (!strcmp(argv[a], "--seed")) seed = strtoull(argv[a + 1], nullptr, 0);
         if (!strcmp(argv[a], "--replay")) replay = argv[a + 1];
         if (!strcmp(argv[a], "--exact")) g_exact = atoi(argv[a + 1]) != 0;
+        if (!strcmp(argv[a], "--dump-band")) {  // SMALL,LARGE: band frames (u32 length + bytes each) to band.bin
+            rng.seed(seed);
+            unsigned small = 0, large = 0;
+            if (sscanf(argv[a + 1], "%u,%u", &small, &large) < 1) return 2;
+            FILE* fp = fopen("band.bin", "wb");
+            if (!fp) return 2;
+            for (unsigned k = 0; k < small + large; k++) {
+                const Bytes f = band_frame(k < small ? 0 : 400);
+                const uint32_t n = (uint32_t)f.size();
+                if (fwrite(&n, 4, 1, fp) != 1 || fwrite(f.data(), 1, n, fp) != n) return 2;
+            }
+            fclose(fp);
+            return 0;
+        }
         if (!strcmp(argv[a], "--dump-ring")) {  // OFF[,BLOCKS,BAD]: a crafted ring frame to ring.zst
             rng.seed(seed);
             unsigned off = 0, nb = 8, bad = 5;
@@ -705,6 +826,7 @@ int main(int argc, char** argv) {
     check_select();
     check_windows();
     check_ring_crafted();
+    check_band(cases / 2 + 1);
     check_ring(cases / 8 + 1);
     check_ncount(cases * 4);
     for (long i = 0; i < cases; i++) {

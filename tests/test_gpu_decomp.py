@@ -496,6 +496,30 @@ def test_zstd_ring_extdict_frames(eng):
     assert (v == abi.V_OK).sum() >= 6 and (v == abi.V_DECOMP_ERROR).sum() >= 2, v
 
 
+def test_zstd_wildcopy_band_frames(eng):
+    """crafted zstd frames (tests/golden/make_zstd_ring.py
+    `band_*`) with a 1 KiB window whose matches, once the ring has wrapped,
+    read the previous segment right past the write position -- where libzstd
+    1.4.9's over-long copies (ZSTD_copy16 / ZSTD_wildcopy of literals and
+    matches, ZSTD_overlapCopy8, ZSTD_safecopy near the ring's end) left bytes
+    that the match then copies.  40 small frames on the lane decoder's ring
+    pass, 4 of 400 blocks on the wave decoder: every verdict, length and byte
+    as the oracle's (the restatement: rpgpu_zstd.h ring_seq; host differential
+    fuzz: tests/native/zstd_fuzz.cpp check_band)."""
+    from redpanda_amd import abi
+
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "zstd_ring.npz"))
+    ends = np.cumsum(g["band_lens"])
+    frames = [g["band_data"][e - n:e].tobytes() for e, n in zip(ends, g["band_lens"])]
+    bs = [batch(f, fmt=WIRE, record_count=1, attrs=4) for f in frames]
+    data, descs = arena(bs, fmt=WIRE, ops=OPS)
+    got = eng.decompress_arena(data, descs)
+    want = compare(got, data, descs)
+    v = want["verdicts"]
+    assert (v == abi.V_OK).sum() >= 20, v
+    assert (got["dres"]["out_cap"][-4:] > 61 + (256 << 10)).all()  # slots for the wave decoder
+
+
 def test_split_fallback_below_wave_size(eng):
     """A corrupt LZ4 frame from C5's arena (batch 126,469 of the bench's seed,
     tests/golden/lz4_split_fallback.npz: 45,806 bytes, two 64 KiB blocks, the
