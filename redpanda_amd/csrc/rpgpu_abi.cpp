@@ -56,7 +56,8 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                              uint64_t out_cap, rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_vres2,
                              rpgpu_record_index* d_index, uint64_t index_cap, uint64_t* d_index_used,
                              void* d_scratch, const uint32_t* d_tables, int grid, uint32_t ws_cap, uint32_t zmode, hipStream_t s,
-                             const Overlap* ov, const DecompStreams* ds);
+                             const Overlap* ov, const DecompStreams* ds, const uint32_t* plan_counts);
+size_t decomp_counter_offset(uint32_t n, uint32_t ws_cap);
 hipError_t launch_uncompress_bound(uint32_t codec, const uint8_t* d_in, uint64_t n, uint64_t* d_res,
                                    hipStream_t s);
 hipError_t launch_uncompress_one(uint32_t codec, const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint64_t cap,
@@ -160,6 +161,12 @@ struct rpgpu_ctx {
     uint64_t max_decoded = RPGPU_DEFAULT_MAX_DECODED_BATCH;  // opts.max_decoded_batch
     uint32_t ws_lanes = 0;  // opts.decomp_ws_lanes (0: the default ceiling)
     uint32_t zmode = 0;     // zstd lane bodies: 0 one-lane, 1 split (LDS), 2 fused + executor
+    // the last decompress plan's queue counters, copied to the host behind it: a run
+    // of that plan (same scratch and n) whose copy has landed skips launches with no work
+    uint32_t* h_plan = nullptr;  // pinned, 64 words
+    hipEvent_t plan_ev = nullptr;
+    const void* plan_scratch = nullptr;
+    uint32_t plan_n = 0;
     int efd = -1;       // rpgpu_eventfd: signalled by a host function after each stage
     std::string err;
 };
@@ -219,7 +226,14 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
     c->grid = c->cu_count * bpc;
     // a blocking stream: it orders after work on the legacy default stream (torch's
     // current stream unless the caller set one), so NULL-stream calls are safe
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess) {
+    // At the higher priority: the decompression's second stream runs beside it, and
+    // its kernels (idle wave decoders included) would otherwise take CUs the main
+    // stream's lane kernels wait for (RPGPU_MAIN_PRIORITY=0: both at the default)
+    int prio_lo = 0, prio_hi = 0;
+    const char* pe = getenv("RPGPU_MAIN_PRIORITY");
+    const bool high = !(pe && pe[0] == '0');
+    if (!high || hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = prio_lo = 0;
+    if (hipStreamCreateWithPriority(&c->stream, hipStreamDefault, prio_hi) != hipSuccess) {
         delete c;
         return nullptr;
     }
@@ -243,6 +257,10 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
     c->zmode = !opts ? 0u : (opts->flags & RPGPU_OPT_ZSTD_SPLIT) ? 1u : (opts->flags & RPGPU_OPT_ZSTD_FUSED) ? 2u : 0u;
     if (opts && (opts->flags & RPGPU_OPT_ZSTD_WAVE_ONLY)) c->zmode |= 4u;  // kZModeNoBlk
     if (!want_overlap) c->have_overlap = false;
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_plan), 64 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&c->plan_ev, hipEventDisableTiming) != hipSuccess) {
+        c->h_plan = nullptr;  // not fatal: every run launches every decoder
+    }
     std::vector<uint32_t> t(rpgpu::kTableWords);
     rpgpu::build_tables(t.data());
     if (hipMalloc(&c->d_tables, sizeof(uint32_t) * t.size()) != hipSuccess ||
@@ -287,6 +305,9 @@ void rpgpu_close(rpgpu_ctx* c) {
         (void)hipStreamSynchronize(c->dstreams.aux2);
         (void)hipStreamDestroy(c->dstreams.aux2);
     }
+    if (c->plan_ev) (void)hipEventSynchronize(c->plan_ev);  // the plan's copy may be on a caller's stream
+    if (c->h_plan) (void)hipHostFree(c->h_plan);
+    if (c->plan_ev) (void)hipEventDestroy(c->plan_ev);
     if (c->dstreams.fork) (void)hipEventDestroy(c->dstreams.fork);
     if (c->dstreams.join) (void)hipEventDestroy(c->dstreams.join);
     if (c->dstreams.join2) (void)hipEventDestroy(c->dstreams.join2);
@@ -491,6 +512,15 @@ int32_t rpgpu_decomp_plan_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, 
     hipError_t e = rpgpu::launch_decomp_plan(d_descs, n, d_data, d_results, d_out_bytes, d_scratch,
                                               c->max_decoded, c->ws_lanes, c->zmode, s);
     if (e != hipSuccess) return fail(c, e, "decomp plan launch");
+    c->plan_scratch = nullptr;
+    if (n && c->h_plan && c->plan_ev) {
+        const uint8_t* cnt = static_cast<const uint8_t*>(d_scratch) + rpgpu::decomp_counter_offset(n, c->ws_lanes);
+        if (hipMemcpyAsync(c->h_plan, cnt, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, s) == hipSuccess &&
+            hipEventRecord(c->plan_ev, s) == hipSuccess) {
+            c->plan_scratch = d_scratch;
+            c->plan_n = n;
+        }
+    }
     return RPGPU_OK;
 }
 
@@ -504,11 +534,16 @@ int32_t rpgpu_decomp_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, u
                      !d_out_results || !d_scratch)))
         return RPGPU_EINVAL;
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    // the plan's counters, when this is a run of the last plan and its copy has landed
+    // (the caller read the plan's output size; no wait here)
+    const uint32_t* pc = nullptr;
+    if (c->plan_scratch == d_scratch && c->plan_n == n && n && hipEventQuery(c->plan_ev) == hipSuccess)
+        pc = c->h_plan;
     hipError_t e = rpgpu::launch_decomp_run(d_descs, n, d_data, d_results, d_dres, d_out, out_cap, d_out_descs,
                                             d_out_results, d_index, d_index ? index_cap : 0, d_index_used,
                                             d_scratch, c->d_tables, c->grid, c->ws_lanes, c->zmode, s,
                                             c->have_overlap ? &c->overlap : nullptr,
-                                            c->have_dstreams ? &c->dstreams : nullptr);
+                                            c->have_dstreams ? &c->dstreams : nullptr, pc);
     if (e != hipSuccess) return fail(c, e, "decomp run launch");
     return RPGPU_OK;
 }

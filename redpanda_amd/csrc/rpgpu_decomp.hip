@@ -96,6 +96,17 @@ uint32_t gzip_lanes(uint32_t n, uint32_t cap) {
 }
 size_t ws_region(uint32_t n, uint32_t cap) { return (size_t)gzip_lanes(n, cap) * sizeof(rpinfl::Ws); }
 uint32_t decomp_waves(uint32_t n) { return n < kDecompWaves ? n : kDecompWaves; }
+// the zstd wave decoder: frames the block-parallel decoder does not plan (corrupt
+// headers, checksums, dictionaries, more blocks than it takes) -- fewer waves: its
+// 256-VGPR, 19 KB-LDS waves, even idle, take CUs from the lane kernels launched
+// beside them (C3 95.2 vs 77.4 ms per step with 2,048; profiles/r5/NOTES.md r5t)
+#ifndef RPGPU_ZSTD_WAVES
+#define RPGPU_ZSTD_WAVES 512
+#endif
+uint32_t zstd_waves(uint32_t n, uint32_t zmode) {
+    const uint32_t w = (zmode & 4) ? kDecompWaves : RPGPU_ZSTD_WAVES;  // kZModeNoBlk: every large frame
+    return n < w ? n : w;
+}
 // scratch: slot[n] u64 | local[n] u64 | block_sum[nb] u64 | validate scratch |
 //          counters (256 B) | wave literal scratch[waves] | lane Ws[lanes]
 // one part of a split body (rpcodec::lz4f_split / snappy_java_split)
@@ -158,9 +169,9 @@ constexpr uint32_t kBlkFrames = 16384, kBlkPool = 65536;
 struct ZbFrame {
     uint32_t first, nblk;  // pool blocks; nblk 0: not planned (the wave decoder's)
     uint64_t lits, recs;   // offsets in the literal / record regions
-    uint64_t fcs, bsm;
+    uint64_t fcs, bsm, oend;
 };
-static_assert(sizeof(ZbFrame) == 40, "ZbFrame layout");
+static_assert(sizeof(ZbFrame) == 48, "ZbFrame layout");
 uint32_t zb_frames(uint32_t n) { return n < kBlkFrames ? n : kBlkFrames; }
 size_t zblk_offset(uint32_t n, uint32_t cap) { return (zseq_offset(n, cap) + zseq_bytes(n) + 255) & ~(size_t)255; }
 size_t zblk_bytes(uint32_t n) {
@@ -214,12 +225,17 @@ Parts parts(void* p, uint32_t n, uint32_t cap) {
 }  // namespace
 
 size_t decomp_scratch_bytes(uint32_t n, uint32_t ws_cap) { return zblk_offset(n, ws_cap) + zblk_bytes(n); }
+size_t decomp_counter_offset(uint32_t n, uint32_t) { return counter_offset(n); }
 
 // slots above this go to the wave decoders (a lane's serial decode of a
 // large body would hold up the whole launch)
 constexpr uint64_t kLaneMaxSlot = 256u << 10;
+// RPGPU_ZSTD_LANE_STREAM 1: the zstd / gzip lane decoders on a third stream,
+// launched first (measured: C5 265.7 vs 236.5 ms -- with GPU_MAX_HW_QUEUES 4 the
+// third stream shares a hardware queue with the main one, so its kernels run
+// before the main stream's instead of beside them; profiles/r5/NOTES.md r5s)
 #ifndef RPGPU_ZSTD_LANE_STREAM
-#define RPGPU_ZSTD_LANE_STREAM 1
+#define RPGPU_ZSTD_LANE_STREAM 0
 #endif
 #ifndef RPGPU_ZSTD_LANE_MAX
 #define RPGPU_ZSTD_LANE_MAX (256u << 10)
@@ -371,10 +387,11 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
         pbase[1] = (uint32_t)(tot >> 32) ? atomicAdd(wcount + 3, (uint32_t)(tot >> 32)) : 0u;
     }
     __syncthreads();
+    uint32_t sc = 0;  // the parts this batch was split into (0: decoded whole)
     if (i < n) {
         slot[i] = over ? (kOverCeiling | need) : sz;
         local[i] = wbase + x - span;
-        uint32_t sf = 0, sc = 0;
+        uint32_t sf = 0;
         if (np) {
             const uint64_t pe = pwbase + y - pspan;  // exclusive prefix within the workgroup
             const uint32_t k0 = (codec == 3 ? pbase[0] + (uint32_t)pe : pbase[1] + (uint32_t)(pe >> 32));
@@ -409,6 +426,15 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
             wlist[n + atomicAdd(wcount + 1, 1u)] = i;
         sfirst[i] = sf;
         scount[i] = sc;
+    }
+    // lane batches of the snappy and gzip decoders (whose kernels walk every batch):
+    // counts only, so a run can skip a launch with nothing to do (counters 12, 13)
+    {
+        const bool sl = i < n && wanted && codec == 2 && (over || sz <= lane_max(2)) && sc == 0;
+        const bool gl = i < n && wanted && codec == 1;
+        const uint64_t sm = __ballot(sl), gm = __ballot(gl);
+        if (l == 0 && sm) atomicAdd(wcount + 10, (uint32_t)__builtin_popcountll(sm));
+        if (l == 0 && gm) atomicAdd(wcount + 11, (uint32_t)__builtin_popcountll(gm));
     }
     // zstd batches for the lane decoder (not wave-owned; overflowing ones too,
     // for their verdict): listed with one atomic per wave
@@ -908,7 +934,7 @@ __global__ __launch_bounds__(256) void zblk_plan_kernel(
     uint32_t* __restrict__ bframe, uint32_t nframes, bool enabled) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nframes || k >= counter[2]) return;
-    ZbFrame f{0, 0, 0, 0, 0, 0};
+    ZbFrame f{0, 0, 0, 0, 0, 0, 0};
     const uint32_t i = wlist[k];
     const rpgpu_batch_desc d = descs[i];
     const rpgpu_batch_result v = vres[i];
@@ -926,6 +952,8 @@ __global__ __launch_bounds__(256) void zblk_plan_kernel(
                 f.recs = atomicAdd(reinterpret_cast<unsigned long long*>(counter + 26), (unsigned long long)pl.recs);
                 f.fcs = pl.fcs;
                 f.bsm = pl.bsm;
+                f.oend = pl.oend;
+                atomicAdd(counter + 29, 1u);
                 rpzstd::plan_blocks(in, body_len(v), cap, pool + first);
                 for (uint32_t j = 0; j < pl.nblk; j++) bframe[first + j] = k;
             } else {
@@ -987,7 +1015,7 @@ __device__ int32_t zblk_run(const uint8_t* in, const ZbFrame& f, const rpzstd::B
     *out_len = 0;
     for (uint32_t j = 0; j < f.nblk; j++) {
         const Blk b = blk[j];
-        const uint64_t room = f.fcs - T;
+        const uint64_t room = f.oend - T;
         if (b.type != 2) {
             if (b.size > room || (b.type == 1 && b.size > f.bsm) || T + b.size > cap) return V_ERROR;
             if (b.type == 0) rpwave::coop_copy(out + T, in + b.in_off, b.size, lid);
@@ -1035,7 +1063,7 @@ __device__ int32_t zblk_run(const uint8_t* in, const ZbFrame& f, const rpzstd::B
         T = o;
     }
     const Blk e = blk[f.nblk - 1];
-    if (T != f.fcs && !(e.type == 0 && e.size == 0)) return V_ERROR;
+    if (f.fcs != kUnknown && T != f.fcs && !(e.type == 0 && e.size == 0)) return V_ERROR;
     *out_len = T;
     return V_OK;
 }
@@ -1355,6 +1383,7 @@ hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const
     // counters 2, 3: wave list lengths; 4, 5: LZ4 / snappy parts; 7: zstd lane list
     if ((e = hipMemsetAsync(p.counter + 2, 0, 4 * sizeof(uint32_t), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(p.counter + 7, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(p.counter + 12, 0, 2 * sizeof(uint32_t), s)) != hipSuccess) return e;
     decomp_caps_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
                                                  max_decoded, p.counter + 2, p.wlist, p.sfirst, p.scount, p.parts,
                                                  part_cap(n));
@@ -1388,9 +1417,20 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                              uint64_t out_cap, rpgpu_batch_desc* d_out_descs, rpgpu_batch_result* d_vres2,
                              rpgpu_record_index* d_index, uint64_t index_cap, uint64_t* d_index_used,
                              void* d_scratch, const uint32_t* d_tables, int grid, uint32_t ws_cap, uint32_t zmode,
-                             hipStream_t s, const Overlap* ov, const DecompStreams* ds) {
+                             hipStream_t s, const Overlap* ov, const DecompStreams* ds, const uint32_t* pc) {
     if (n == 0) return d_index_used ? hipMemsetAsync(d_index_used, 0, sizeof(uint64_t), s) : hipSuccess;
     const Parts p = parts(d_scratch, n, ws_cap);
+    // pc: the plan's counters on the host (rpgpu_abi.cpp), or null -- then every
+    // decoder is launched.  With them, decoders with nothing to do are not: idle
+    // waves still take registers and LDS from the kernels running beside them.
+    auto c64 = [&](int k) { return (uint64_t)pc[k] | ((uint64_t)pc[k + 1] << 32); };
+    const bool parts3 = !pc || pc[4] != 0, parts2 = !pc || pc[5] != 0;
+    const bool blk_any = !pc || pc[28] != 0;
+    const bool blk_fits = pc && c64(32) + (c64(26) + 16) * 8 <= out_cap;
+    const bool zwave_any = !pc || pc[2] > (blk_fits ? pc[29] : 0u);
+    const bool lzwave_any = !pc || pc[6] != 0 || parts3 || parts2;  // split fallbacks join the LZ list
+    const bool zlane_any = !pc || pc[7] != 0;
+    const bool snappy_any = !pc || pc[12] != 0, gzip_any = !pc || pc[13] != 0;
     const uint32_t nblk = (n + 255) / 256;
     decomp_counters_kernel<<<1, 64, 0, s>>>(p.counter, 1);
     hipError_t e = hipGetLastError();
@@ -1409,7 +1449,7 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
 #endif
     }
     // the zstd / gzip lane decoders (on zs)
-    auto zlanes = [&]() -> hipError_t {
+    auto zlanes_zstd = [&]() -> hipError_t {
         hipError_t e = hipSuccess;
         const uint32_t zl = zstd_lanes(n, ws_cap);  // the HBM-workspace lane decoder (at most zl lanes)
         // the split decoder over the zstd lane batches it planned: A1 literals, A2
@@ -1451,11 +1491,18 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
         zstd_ring_kernel<<<(zl + 255) / 256, 256, 0, zs>>>(d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres,
                                                           d_out, out_cap, d_out_descs, p.counter, p.wlist + 2 * (size_t)n);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        const uint32_t gl = gzip_lanes(n, ws_cap);
-        ws_lane_kernel<1><<<(gl + 255) / 256, 256, 0, zs>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
-                                                             d_dres, d_out, out_cap, d_out_descs, p.gws, p.counter,
-                                                             nullptr, nullptr);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+        return hipSuccess;
+    };
+    auto zlanes = [&]() -> hipError_t {
+        hipError_t e = hipSuccess;
+        if (zlane_any && (e = zlanes_zstd()) != hipSuccess) return e;
+        if (gzip_any) {
+            const uint32_t gl = gzip_lanes(n, ws_cap);
+            ws_lane_kernel<1><<<(gl + 255) / 256, 256, 0, zs>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
+                                                                 p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.gws,
+                                                                 p.counter, nullptr, nullptr);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
         return hipSuccess;
     };
 #if RPGPU_ZSTD_LANE_STREAM
@@ -1469,17 +1516,19 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     // main stream's lane launches got shorter and the snappy parts moved over
     // from the second stream, which the zstd wave decoder keeps the longer one.
     const uint32_t pgrid = (part_cap(n) / 2 < 65536u ? part_cap(n) / 2 + 255 : 65536u + 255) / 256;
-    part_kernel<3><<<pgrid, 256, 0, s>>>(p.parts, p.counter + 4, part_cap(n), d_descs, d_data, p.slot, p.local,
-                                         p.block_sum, d_out, out_cap, p.pres);
-    part_kernel<2><<<pgrid, 256, 0, s>>>(p.parts, p.counter + 5, part_cap(n), d_descs, d_data, p.slot, p.local,
-                                         p.block_sum, d_out, out_cap, p.pres);
+    if (parts3)
+        part_kernel<3><<<pgrid, 256, 0, s>>>(p.parts, p.counter + 4, part_cap(n), d_descs, d_data, p.slot, p.local,
+                                             p.block_sum, d_out, out_cap, p.pres);
+    if (parts2)
+        part_kernel<2><<<pgrid, 256, 0, s>>>(p.parts, p.counter + 5, part_cap(n), d_descs, d_data, p.slot, p.local,
+                                             p.block_sum, d_out, out_cap, p.pres);
     if (ds) {
         if ((e = hipEventRecord(ds->parts, s)) != hipSuccess) return e;
     }
     // zstd frames above kZstdLaneMaxSlot on the second stream: block-parallel
     // (entropy stages per block, then one wave per frame), the rest by the wave decoder
     const ZbParts zb = zbparts(d_scratch, n, ws_cap);
-    {
+    if (blk_any) {
         const ZbLaunch zq = zblk_launch();
         zblk_entropy_kernel<<<zq.grid, 64, zq.lanes * sizeof(ZbWs), ws>>>(d_descs, d_data, p.counter, p.wlist, zb.frames,
                                                                        zb.pool, zb.bframe, d_out, out_cap, zq.lanes);
@@ -1488,27 +1537,35 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                                                       out_cap, d_out_descs, p.counter, p.wlist, zb.frames, zb.pool);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    decomp_wave_kernel<kFamZstd><<<decomp_waves(n), 64, sizeof(rpzstd::Ws), ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
-                                                                p.block_sum, d_dres, d_out, out_cap, d_out_descs,
-                                                                p.counter + 1, p.lits, p.wlist, p.counter + 2,
-                                                                zb.frames, p.counter);
+    if (zwave_any)
+        decomp_wave_kernel<kFamZstd><<<zstd_waves(n, zmode), 64, sizeof(rpzstd::Ws), ws>>>(
+            d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.counter + 1,
+            p.lits, p.wlist, p.counter + 2, zb.frames, p.counter);
     if (ds) {
         if ((e = hipStreamWaitEvent(ws, ds->parts, 0)) != hipSuccess) return e;
     }
-    split_finish_kernel<<<nblk, 256, 0, ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, p.sfirst,
-                                              p.scount, p.pres, d_dres, d_out, out_cap, d_out_descs, p.counter + 3,
-                                              p.wlist);
+    if (parts3 || parts2)
+        split_finish_kernel<<<nblk, 256, 0, ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, p.sfirst,
+                                                  p.scount, p.pres, d_dres, d_out, out_cap, d_out_descs, p.counter + 3,
+                                                  p.wlist);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    decomp_wave_kernel<kFamLz><<<decomp_waves(n), 64, 0, ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
-                                                              p.block_sum, d_dres, d_out, out_cap, d_out_descs,
-                                                              p.counter, p.lits, p.wlist + n, p.counter + 3, nullptr,
-                                                              nullptr);
+    if (lzwave_any)
+        decomp_wave_kernel<kFamLz><<<decomp_waves(n), 64, 0, ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
+                                                                  p.block_sum, d_dres, d_out, out_cap, d_out_descs,
+                                                                  p.counter, p.lits, p.wlist + n, p.counter + 3,
+                                                                  nullptr, nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t lzb = (n + 255) / 256;
     decomp_lane_kernel<3><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
                                               out_cap, d_out_descs, p.scount);
-    decomp_lane_kernel<2><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
-                                              out_cap, d_out_descs, p.scount);
+    // snappy lanes on the second stream after its wave decoders (C5: the main stream
+    // carries the part kernels, the LZ4 lanes and the zstd lanes, the longer chain)
+#ifndef RPGPU_SNAPPY_LANE_AUX
+#define RPGPU_SNAPPY_LANE_AUX 1
+#endif
+    if (snappy_any)
+        decomp_lane_kernel<2><<<lzb, 256, 0, RPGPU_SNAPPY_LANE_AUX ? ws : s>>>(
+            d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.scount);
     if ((e = hipGetLastError()) != hipSuccess) return e;
 #if !RPGPU_ZSTD_LANE_STREAM
     if ((e = zlanes()) != hipSuccess) return e;

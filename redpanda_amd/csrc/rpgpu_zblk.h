@@ -31,9 +31,11 @@
 //
 // Only frames where this is exactly the serial decode take it (P's
 // eligibility): a body that is one complete frame, no dictionary, no
-// checksum, a known content size above the 64 KiB staging buffer (the
-// streaming path) that the ring buffer holds whole (no wrap), every block
-// present, at most kBlkMax blocks, every header parseable.  For those every
+// checksum, streamed (a content size above the 64 KiB staging buffer, or none:
+// the Java client's frames) through a ring buffer that never wraps for it
+// (holds the content size, or, without one, the bound of every block before
+// the last plus a block), every block present, at most kBlkMax blocks, every
+// header parseable.  For those every
 // failure of any block is RPGPU_V_DECOMP_ERROR whichever check finds it
 // (rpgpu_zstd.h: block errors in the streaming path, the slot bound checked
 // against the plan's), so the stages may find them in any order.  Everything
@@ -73,6 +75,7 @@ constexpr uint64_t kRepFlag = 1ull << 27;
 struct BlkPlan {
     uint32_t nblk;
     uint64_t fcs, bsm, lits, recs;
+    uint64_t oend;  // the ring buffer's size (the content size when known): each block's room is oend - T
     bool ok;
 };
 
@@ -80,21 +83,26 @@ struct BlkPlan {
 // counts), or ok = false.  cap: the slot's decoded capacity; the path needs bound() <= cap (then a slot overflow is an error,
 // as uncompress() decides it, like every other failure).
 RPC_HD BlkPlan plan_blocks(const uint8_t* in, uint64_t n, uint64_t cap, Blk* blk) {
-    BlkPlan r{0, 0, 0, 0, 0, false};
+    BlkPlan r{0, 0, 0, 0, 0, 0, false};
     uint64_t bnd = 0;  // bound(in, n) for such a body: the blocks' sum
     if (n < 5 || le32(in) != kMagic) return r;
     Frame h;
-    if (frame_header(in, n, h) != 0 || h.dict || h.csum || h.fcs == kUnknown || h.fcs <= kStage) return r;
+    if (frame_header(in, n, h) != 0 || h.dict || h.csum) return r;
+    const bool known = h.fcs != kUnknown;
+    if (known && h.fcs <= kStage) return r;  // the single-pass path's
     const uint64_t win = h.window < 1024 ? 1024 : h.window;
     if (win > kMaxWindow) return r;
+    const uint64_t ring = win + (win < kBlockMax ? win : kBlockMax) + 64;
     {
         const uint64_t need_in = h.bsm < 4 ? 4 : h.bsm;
-        const uint64_t ring = win + (win < kBlockMax ? win : kBlockMax) + 64;
-        if (ring < h.fcs) return r;  // the ring would wrap
-        if (need_in + h.fcs > kBudget) return r;
+        if (known && ring < h.fcs) return r;  // the ring would wrap
+        const uint64_t need_out = known ? h.fcs : ring;
+        if (need_in + need_out > kBudget) return r;
+        r.oend = need_out;
     }
     r.fcs = h.fcs;
     r.bsm = h.bsm;
+    uint64_t bnd_prev = 0;  // the bound before the last block: no wrap after any earlier one
     int32_t last_huf = -1, last_t[3] = {-1, -1, -1};
     bool fse_set = false;
     uint64_t ip = h.hsize;
@@ -207,8 +215,12 @@ RPC_HD BlkPlan plan_blocks(const uint8_t* in, uint64_t n, uint64_t cap, Blk* blk
         if (blk) blk[r.nblk] = b;
         r.nblk++;
         ip += cb;
+        if (!last) bnd_prev = bnd;
     }
     if (ip != n || bnd > cap) return r;  // exactly one frame
+    // unknown content size: the ring (window + block + 64) wraps once a block might
+    // not fit behind what the blocks before produced -- never, if their bound leaves room
+    if (!known && bnd_prev + h.bsm > ring) return r;
     r.ok = true;
     return r;
 }
@@ -303,7 +315,7 @@ RPC_HD int32_t blk_resolve(const Blk* blk, const BlkPlan& p, uint64_t* recs, uin
     *out_len = 0;
     for (uint32_t k = 0; k < p.nblk; k++) {
         const Blk& b = blk[k];
-        const uint64_t room = p.fcs - T;  // the ring's room (no wrap on this path)
+        const uint64_t room = p.oend - T;  // the ring's room (no wrap on this path)
         if (b.type != 2) {  // raw / RLE: the ring's room, the block maximum, the slot
             if (b.size > room || (b.type == 1 && b.size > p.bsm) || T + b.size > cap) return V_ERROR;
             T += b.size;
@@ -363,7 +375,7 @@ RPC_HD int32_t blk_resolve(const Blk* blk, const BlkPlan& p, uint64_t* recs, uin
     // the content size is checked at the last block unless it is an empty raw
     // block (its header carries no bytes: the streaming loop skips the check)
     const Blk& e = blk[p.nblk - 1];
-    if (T != p.fcs && !(e.type == 0 && e.size == 0)) return V_ERROR;
+    if (p.fcs != kUnknown && T != p.fcs && !(e.type == 0 && e.size == 0)) return V_ERROR;
     *out_len = T;
     return V_OK;
 }

@@ -44,11 +44,16 @@
 //     kept flat here and such a match is rebuilt from it (block(): vstart /
 //     pstart).  Valid frames never reach either (offsets <= window).
 //
-// Not restated: libzstd's copies write up to 32-48 bytes past their end
-// (ZSTD_wildcopy / ZSTD_overlapCopy8), into the ring; an offset beyond the
-// window whose match reads the previous segment within 64 bytes past the
-// current write position reads those bytes in libzstd and the previous
-// segment's here (tests/native/zstd_fuzz.cpp in_overrun_band).
+//   * libzstd's copies write past their end into the ring (ZSTD_copy16 +
+//     ZSTD_wildcopy for literals, ZSTD_wildcopy or ZSTD_overlapCopy8 + 8-byte
+//     steps for matches, ZSTD_safecopy within 32 bytes of the ring's end); a
+//     match that reads the previous segment just past the current write
+//     position reads those bytes (ring_seq: the bytes past the write position
+//     are tracked as runs of their sources; tests/native/zstd_fuzz.cpp
+//     check_band against libzstd, tests/golden/zstd_ring.npz band_*).  Not
+//     modelled: a match spanning the previous segment's end into the current
+//     one within 16 bytes of the segment's start (libzstd's ZSTD_wildcopy then
+//     reads bytes the copy has not written yet) -- corrupt frames only.
 //
 // Serial per frame: the same code runs on the host in the differential fuzz
 // (tests/native/zstd_fuzz.cpp) and on the device in one lane per batch, each

@@ -612,16 +612,35 @@ def large_mutated_zstd(rng, n):
     return out
 
 
-@pytest.mark.parametrize("case", ["large", "mutated"])
+def drop_content_size(frame: bytes) -> bytes:
+    """The same zstd frame without its content size (as the Java client's
+    streaming compressor writes them): a window descriptor of 2^ceil(log2 fcs)
+    instead of single-segment mode; the blocks unchanged."""
+    fhd = frame[4]
+    did, ss, fid = fhd & 3, (fhd >> 5) & 1, fhd >> 6
+    dsz = [0, 1, 2, 4][did]
+    fsz = [ss, 2, 4, 8][fid]
+    pos = 5 + (0 if ss else 1)
+    wd = bytes([frame[5]]) if not ss else b""
+    dict_id = frame[pos:pos + dsz]
+    fcs = int.from_bytes(frame[pos + dsz:pos + dsz + fsz], "little") + (256 if fid == 1 else 0)
+    if ss:
+        e = max(10, (fcs - 1).bit_length())
+        wd = bytes([(e - 10) << 3])
+    return frame[:4] + bytes([fhd & 0x1F & ~0x20]) + wd + dict_id + frame[pos + dsz + fsz:]
+
+
+@pytest.mark.parametrize("case", ["large", "mutated", "no_content_size"])
 def test_zstd_block_parallel(case):
     """Large zstd frames decoded block-parallel (rpgpu_zblk.h: the blocks'
     literals and sequences by separate lanes, repeat offsets resolved by a wave
     scan, one wave executing each frame) against the oracle, and byte for byte
     against the one-wave decoder (RPGPU_OPT_ZSTD_WAVE_ONLY) on the same arena:
     verdicts, lengths, rewritten batches, index.  Cases: C5-shaped bodies of
-    200 KiB - 1 MiB with 1 % corrupted batches, and library frames of 2-8
-    blocks mutated (errors found by any stage in any block).  The plan's
-    output holds the block decoder's literal and record regions."""
+    200 KiB - 1 MiB with 1 % corrupted batches, library frames of 2-8 blocks
+    mutated (errors found by any stage in any block), and frames without a
+    content size (the Java client's kind: the ring's room instead).  The
+    plan's output holds the block decoder's literal and record regions."""
     from redpanda_amd import abi, engine
 
     if case == "large":
@@ -629,9 +648,17 @@ def test_zstd_block_parallel(case):
                                 body_max=1 << 20, ops=abi.OPS_PRODUCE | abi.OP_DECOMP, payload=abi.PAYLOAD_TEXT,
                                 corrupt_ppm=10_000, corrupt_mask=0x3FF)
         data, descs = engine.build_arena(spec, 400)
-    else:
+    elif case == "mutated":
         rng = np.random.default_rng(0xB02)
         bs = [batch(c, fmt=WIRE, record_count=rc, attrs=4) for c, rc in large_mutated_zstd(rng, 120)]
+        data, descs = arena(bs, fmt=WIRE, ops=OPS)
+    else:
+        rng = np.random.default_rng(0xB03)
+        bs = []
+        for i in range(60):
+            recs = records(rng, int(rng.integers(250, 900)), 8, 1100, text=bool(i % 3))
+            bs.append(batch(drop_content_size(orc.compress(4, b"".join(recs))), fmt=WIRE, record_count=len(recs),
+                            attrs=4))
         data, descs = arena(bs, fmt=WIRE, ops=OPS)
     with engine.Engine(0) as e:
         got = e.decompress_arena(data, descs)
