@@ -260,6 +260,87 @@ RPC_HD int32_t blk_literals(const uint8_t* in, const Blk* blk, uint32_t k, uint8
 
 // E2.  The sequences of block k as raw records at recs + blk[k].rec_out: ll
 // << 28 | ml << 46 | offset field.  Returns 0 or -1.
+//
+// While at least 60 bytes of the stream remain below the read point, bits come
+// from a 256-bit register window with the 16 bytes below it loaded one slide
+// ahead (FastBits): a sequence never waits on memory for its bits.  The rest
+// of the stream goes through the exact reader (rpgpu_zstd.h Bits: libzstd's
+// over-read behaviour near the stream's start).
+struct FastBits {
+    const uint8_t* s;
+    int64_t pos;   // bits below the read point (Bits::pos)
+    int64_t base;  // the window: stream bytes [base, base + 32)
+    uint64_t q0, q1, q2, q3, p0, p1;  // window words (q0 lowest), then [base - 16, base)
+};
+constexpr int64_t kFastMin = 480;  // fast while pos >= this: every slide's prefetch stays in the stream
+RPC_HD void fb_init(FastBits& f, const uint8_t* s, int64_t pos) {
+    f.s = s;
+    f.pos = pos;
+    f.base = ((pos + 7) >> 3) - 32;  // the read point in the window's top byte
+    f.q0 = le64(s + f.base);
+    f.q1 = le64(s + f.base + 8);
+    f.q2 = le64(s + f.base + 16);
+    f.q3 = le64(s + f.base + 24);
+    f.p0 = le64(s + f.base - 16);
+    f.p1 = le64(s + f.base - 8);
+}
+// fewer than 96 bits (one sequence's most) left in the window below the read
+// point: the window moves 16 bytes down onto the prefetched words
+RPC_HD void fb_slide(FastBits& f) {
+    if (f.pos - 8 * f.base < 96) {
+        f.q3 = f.q1;
+        f.q2 = f.q0;
+        f.q1 = f.p1;
+        f.q0 = f.p0;
+        f.base -= 16;
+        const int64_t pb = f.base - 16 > 0 ? f.base - 16 : 0;
+        f.p0 = le64(f.s + pb);
+        f.p1 = le64(f.s + pb + 8);
+    }
+}
+RPC_HD uint64_t fb_read(FastBits& f, uint32_t n) {
+    const int64_t lo = f.pos - (int64_t)n;
+    const uint32_t o = (uint32_t)(lo - 8 * f.base), sh = o & 63;
+    // the word at bit o and the next, by the bits of o (selects: an indexed form
+    // of the four words went to scratch memory)
+    const bool h64 = (o & 64) != 0, h128 = (o & 128) != 0;
+    const uint64_t a0 = h64 ? f.q1 : f.q0, b0 = h64 ? f.q2 : f.q1;
+    const uint64_t a1 = h64 ? f.q3 : f.q2, b1 = h64 ? 0 : f.q3;
+    const uint64_t a = h128 ? a1 : a0, b = h128 ? b1 : b0;
+    const uint64_t v = sh ? (a >> sh) | (b << (64 - sh)) : a;
+    f.pos = lo;
+    return v & lomask(n);
+}
+// the two readers: the exact one (BIT_readBits / BIT_readBitsFast) and the window's
+RPC_HD uint64_t sq_rd(Bits& b, uint32_t n) { return read_bits(b, n); }
+RPC_HD uint64_t sq_rdf(Bits& b, uint32_t n) { return read_bits_fast(b, n); }
+RPC_HD uint64_t sq_rd(FastBits& f, uint32_t n) { return fb_read(f, n); }
+RPC_HD uint64_t sq_rdf(FastBits& f, uint32_t n) { return fb_read(f, n); }
+// one sequence (ZSTD_decodeSequence's order of reads), its raw record
+template <class R, class W>
+RPC_HD uint64_t seq_record(R& r, const W& w, uint32_t& sLL, uint32_t& sOF, uint32_t& sML) {  // R: Bits / FastBits
+    const uint32_t eLL = fse_cell(w.ll, w.ll_log, sLL), eML = fse_cell(w.ml, w.ml_log, sML),
+                   eOF = fse_cell(w.of, w.of_log, sOF);
+    const uint32_t cLL = eLL & 0xFF, cML = eML & 0xFF, cOF = eOF & 0xFF;
+    const uint32_t llBits = kLLBits[cLL], mlBits = kMLBits[cML];
+    uint64_t of;
+    if (cOF > 1) {
+        const uint64_t v = (uint64_t)((1u << cOF) - 3u) + sq_rdf(r, cOF);
+        of = v < kRepFlag ? v : kRepFlag - 1;  // beyond any frame position: R rejects it either way
+    } else if (cOF == 0) {
+        of = kRepFlag;
+    } else {
+        of = kRepFlag | (1u + (kLLBase[cLL] == 0) + (uint32_t)sq_rdf(r, 1));
+    }
+    uint64_t ml = kMLBase[cML];
+    if (mlBits) ml += sq_rdf(r, mlBits);
+    uint64_t ll = kLLBase[cLL];
+    if (llBits) ll += sq_rdf(r, llBits);
+    sLL = (eLL >> 16) + (uint32_t)sq_rd(r, (eLL >> 8) & 0xFF);
+    sML = (eML >> 16) + (uint32_t)sq_rd(r, (eML >> 8) & 0xFF);
+    sOF = (eOF >> 16) + (uint32_t)sq_rd(r, (eOF >> 8) & 0xFF);
+    return of | (ll << 28) | (ml << 46);
+}
 template <class W>
 RPC_HD int32_t blk_sequences(const uint8_t* in, const Blk* blk, uint32_t k, uint64_t* recs, W& w) {
     const Blk& b = blk[k];
@@ -279,29 +360,25 @@ RPC_HD int32_t blk_sequences(const uint8_t* in, const Blk* blk, uint32_t k, uint
     uint32_t sOF = (uint32_t)read_bits(bt, w.of_log);
     uint32_t sML = (uint32_t)read_bits(bt, w.ml_log);
     uint64_t* o = recs + b.rec_out;
-    for (uint32_t q = 0; q < b.nseq; q++) {
-        const uint32_t eLL = fse_cell(w.ll, w.ll_log, sLL), eML = fse_cell(w.ml, w.ml_log, sML),
-                       eOF = fse_cell(w.of, w.of_log, sOF);
-        const uint32_t cLL = eLL & 0xFF, cML = eML & 0xFF, cOF = eOF & 0xFF;
-        const uint32_t llBits = kLLBits[cLL], mlBits = kMLBits[cML];
-        uint64_t of;
-        if (cOF > 1) {
-            const uint64_t v = (uint64_t)((1u << cOF) - 3u) + read_bits_fast(bt, cOF);
-            of = v < kRepFlag ? v : kRepFlag - 1;  // beyond any frame position: R rejects it either way
-        } else if (cOF == 0) {
-            of = kRepFlag;
-        } else {
-            of = kRepFlag | (1u + (kLLBase[cLL] == 0) + (uint32_t)read_bits_fast(bt, 1));
+    uint32_t q = 0;
+#ifndef RPZB_NO_FASTBITS
+    if (bt.pos >= kFastMin + 96) {
+        FastBits f;
+        fb_init(f, bt.s, bt.pos);
+        for (; q < b.nseq && f.pos >= kFastMin; q++) {
+            fb_slide(f);
+#ifdef RPZB_DIAG_NOREC  // diagnostics build: records not stored (timing only)
+            const uint64_t x = seq_record(f, w, sLL, sOF, sML);
+            if (x == 12345) o[0] = x;
+#else
+            o[q] = seq_record(f, w, sLL, sOF, sML);
+#endif
         }
-        uint64_t ml = kMLBase[cML];
-        if (mlBits) ml += read_bits_fast(bt, mlBits);
-        uint64_t ll = kLLBase[cLL];
-        if (llBits) ll += read_bits_fast(bt, llBits);
-        sLL = (eLL >> 16) + (uint32_t)read_bits(bt, (eLL >> 8) & 0xFF);
-        sML = (eML >> 16) + (uint32_t)read_bits(bt, (eML >> 8) & 0xFF);
-        sOF = (eOF >> 16) + (uint32_t)read_bits(bt, (eOF >> 8) & 0xFF);
-        o[q] = of | (ll << 28) | (ml << 46);
+        bt.pos = f.pos;
+        bt.wb = -64;  // the exact reader's window reloads at its next read
     }
+#endif
+    for (; q < b.nseq; q++) o[q] = seq_record(bt, w, sLL, sOF, sML);
     if (bt.pos > 0) return -1;  // BIT_reloadDStream < BIT_DStream_completed
     return 0;
 }
