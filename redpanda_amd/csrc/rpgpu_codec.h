@@ -1118,12 +1118,16 @@ RPC_HD bool snappy_raw(E& em, const uint8_t* in, uint64_t n, uint8_t* out, uint3
 // 16 bytes of `expected` (a split chunk's output ends there: the next chunk's
 // follows).  Acceptance is snappy_raw's, check for check.  `lim` = bytes of
 // `in` that may be read.  Host-compiled by tests/native/codec_fuzz.cpp.
-#ifdef __HIPCC__
-static __host__ __device__ __attribute__((noinline))
-#else
-static inline
+// Opt-in (RPGPU_SNAPPY_LANE=1): measured slower than snappy_raw on C5 (parts
+// 102 vs 65 ms, lanes 39 vs 18 ms: snappy's elements are shorter than LZ4's
+// sequences and the fused form's selects cost more than the loads they save).
+// Inlined: out of line (flat pointers) its loads of bytes it had just stored
+// came back stale on the device (a C5 snappy-java body's parts; round 5's
+// split zstd executor showed the same, profiles/r5/NOTES.md r5c-r5i).
+#ifndef RPGPU_SNAPPY_LANE
+#define RPGPU_SNAPPY_LANE 0
 #endif
-bool snappy_raw_lane(const uint8_t* in, int32_t n, uint8_t* out, int32_t expected, int32_t hdr, int32_t lim) {
+RPC_HD bool snappy_raw_lane(const uint8_t* in, int32_t n, uint8_t* out, int32_t expected, int32_t hdr, int32_t lim) {
     int32_t ip = hdr, op = 0;
     const int32_t oend = expected;
     Win64 W;
@@ -1303,7 +1307,7 @@ RPC_HD int32_t snappy_raw_append(E& em, const uint8_t* in, uint64_t n, uint8_t* 
     if (!snappy_varint(in, n, ulen, used)) return V_ERROR;
     if (zero_skip && ulen == 0) return V_OK;
     if (o + ulen > cap) return V_OVERFLOW;
-    if constexpr (IsLane<E>::value) {
+    if constexpr (IsLane<E>::value && RPGPU_SNAPPY_LANE) {
         // the input is readable kInPad bytes past the chunk (the next chunk, the arena's pad)
         if (!snappy_raw_lane(in, (int32_t)n, out + o, (int32_t)ulen, (int32_t)used, (int32_t)(n + kInPad)))
             return V_ERROR;
@@ -1441,13 +1445,13 @@ RPC_HD int64_t decode_part(uint32_t kind, const uint8_t* in, uint64_t in_len, ui
         copy_exact(out, in, in_len);
         return (int64_t)in_len;
     }
-#ifdef RPGPU_SNAPPY_PART_PLAIN  // the plain decoder (A/B builds)
-    BoundEmit em{out + out_cap};
-    return snappy_raw(em, in, in_len, out, (uint32_t)out_cap, hdr) ? (int64_t)out_cap : -1;
-#else
+#if RPGPU_SNAPPY_LANE
     return snappy_raw_lane(in, (int32_t)in_len, out, (int32_t)out_cap, (int32_t)hdr, (int32_t)(in_len + kInPad))
                ? (int64_t)out_cap
                : -1;
+#else
+    BoundEmit em{out + out_cap};
+    return snappy_raw(em, in, in_len, out, (uint32_t)out_cap, hdr) ? (int64_t)out_cap : -1;
 #endif
 }
 // The serial decoder's verdict for a planned body from its parts' decoded

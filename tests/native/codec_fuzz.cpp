@@ -433,6 +433,20 @@ int main(int argc, char** argv) {
         if (!strcmp(argv[a], "--cases")) cases = atol(argv[a + 1]);
         if (!strcmp(argv[a], "--seed")) seed = strtoull(argv[a + 1], nullptr, 0);
         if (!strcmp(argv[a], "--exact")) g_exact = atoi(argv[a + 1]) != 0;
+        if (!strcmp(argv[a], "--replay")) {  // CODEC:FILE -- one body, checked every way
+            int codec = 0;
+            char path[4096];
+            if (sscanf(argv[a + 1], "%d:%4095s", &codec, path) != 2) return 2;
+            FILE* fp = fopen(path, "rb");
+            if (!fp) return 2;
+            Bytes in;
+            int ch;
+            while ((ch = fgetc(fp)) != EOF) in.push_back((uint8_t)ch);
+            fclose(fp);
+            check(codec, in, "replay", 0);
+            printf("replay: engine == oracle\n");
+            return 0;
+        }
     }
     rng.seed(seed);
     for (long c = 0; c < cases; c++) {

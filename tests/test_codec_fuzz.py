@@ -11,12 +11,12 @@ ROOT = Path(__file__).resolve().parents[1]
 CONDA = "/opt/conda"
 
 
-def build_fuzzer(tmp: Path) -> Path:
+def build_fuzzer(tmp: Path, defines: tuple = ()) -> Path:
     import oracle.oracle as orc
 
     lib = orc.build()
-    exe = tmp / "codec_fuzz"
-    subprocess.run(["g++", "-O2", "-std=c++17", f"-I{ROOT / 'redpanda_amd' / 'csrc'}",
+    exe = tmp / ("codec_fuzz" + "".join("_" + d.replace("=", "_") for d in defines))
+    subprocess.run(["g++", "-O2", "-std=c++17", *[f"-D{d}" for d in defines], f"-I{ROOT / 'redpanda_amd' / 'csrc'}",
                     f"-I{ROOT / 'include'}", f"-I{CONDA}/include",
                     str(ROOT / "tests" / "native" / "codec_fuzz.cpp"), "-o", str(exe),
                     f"-L{lib.parent}", "-lrporacle", f"-Wl,-rpath,{lib.parent}",
@@ -32,3 +32,12 @@ def test_codec_restatement_matches_oracle(tmp_path):
                            capture_output=True, text=True, timeout=900)
         assert r.returncode == 0, r.stderr[-6000:]
         assert "engine == oracle" in r.stdout
+
+
+def test_snappy_lane_decoder_matches_oracle(tmp_path):
+    """The opt-in lane-form snappy decoder (RPGPU_SNAPPY_LANE=1, rpgpu_codec.h
+    snappy_raw_lane) for lane batches and snappy-java parts: same checks."""
+    exe = build_fuzzer(tmp_path, ("RPGPU_SNAPPY_LANE=1",))
+    r = subprocess.run([str(exe), "--cases", "15000", "--seed", "13"], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-6000:]
+    assert "engine == oracle" in r.stdout
