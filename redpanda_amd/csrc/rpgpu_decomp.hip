@@ -1525,16 +1525,16 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     if (ds) {
         if ((e = hipEventRecord(ds->parts, s)) != hipSuccess) return e;
     }
-    // the LZ4 lanes (which also finish every batch nobody decodes) are submitted
-    // before the second stream's kernels: C3's 1,024 lane workgroups fill the GPU
-    // at once, and the second stream's idle decoders, dispatched first, kept some
-    // of them waiting (C3 ~93 vs ~77 ms per step)
-    decomp_lane_kernel<3><<<(n + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
-                                                          d_dres, d_out, out_cap, d_out_descs, p.scount);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    // zstd frames above kZstdLaneMaxSlot on the second stream: block-parallel
-    // (entropy stages per block, then one wave per frame), the rest by the wave decoder
+    // zstd frames above kZstdLaneMaxSlot on the second stream: the wave decoder for
+    // the frames the block-parallel decoder does not take -- first: idle, its waves
+    // leave before C3's lane workgroups fill the GPU (launched behind the block
+    // decoder's kernels they waited beside them and slowed them, 92 vs 78 ms) --
+    // then block-parallel (entropy stages per block, then one wave per frame)
     const ZbParts zb = zbparts(d_scratch, n, ws_cap);
+    if (zwave_any)
+        decomp_wave_kernel<kFamZstd><<<zstd_waves(n, zmode), 64, sizeof(rpzstd::Ws), ws>>>(
+            d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.counter + 1,
+            p.lits, p.wlist, p.counter + 2, zb.frames, p.counter);
     if (blk_any) {
         const ZbLaunch zq = zblk_launch();
         zblk_entropy_kernel<<<zq.grid, 64, zq.lanes * sizeof(ZbWs), ws>>>(d_descs, d_data, p.counter, p.wlist, zb.frames,
@@ -1544,10 +1544,6 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                                                       out_cap, d_out_descs, p.counter, p.wlist, zb.frames, zb.pool);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if (zwave_any)
-        decomp_wave_kernel<kFamZstd><<<zstd_waves(n, zmode), 64, sizeof(rpzstd::Ws), ws>>>(
-            d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.counter + 1,
-            p.lits, p.wlist, p.counter + 2, zb.frames, p.counter);
     if (ds) {
         if ((e = hipStreamWaitEvent(ws, ds->parts, 0)) != hipSuccess) return e;
     }
@@ -1563,6 +1559,8 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                                                                   nullptr, nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t lzb = (n + 255) / 256;
+    decomp_lane_kernel<3><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
+                                              out_cap, d_out_descs, p.scount);
     // snappy lanes on the second stream after its wave decoders (C5: the main stream
     // carries the part kernels, the LZ4 lanes and the zstd lanes, the longer chain)
 #ifndef RPGPU_SNAPPY_LANE_AUX
