@@ -247,6 +247,7 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
                        hipEventCreateWithFlags(&c->dstreams.fork, hipEventDisableTiming) == hipSuccess &&
                        hipEventCreateWithFlags(&c->dstreams.join, hipEventDisableTiming) == hipSuccess &&
                        hipEventCreateWithFlags(&c->dstreams.join2, hipEventDisableTiming) == hipSuccess &&
+                       hipEventCreateWithFlags(&c->dstreams.lanes, hipEventDisableTiming) == hipSuccess &&
                        hipEventCreateWithFlags(&c->dstreams.parts, hipEventDisableTiming) == hipSuccess;
     c->have_overlap = hipStreamCreateWithFlags(&c->overlap.aux, hipStreamNonBlocking) == hipSuccess;
     for (int k = 0; c->have_overlap && k <= c->overlap.chunks; k++)
@@ -311,6 +312,7 @@ void rpgpu_close(rpgpu_ctx* c) {
     if (c->dstreams.fork) (void)hipEventDestroy(c->dstreams.fork);
     if (c->dstreams.join) (void)hipEventDestroy(c->dstreams.join);
     if (c->dstreams.join2) (void)hipEventDestroy(c->dstreams.join2);
+    if (c->dstreams.lanes) (void)hipEventDestroy(c->dstreams.lanes);
     if (c->dstreams.parts) (void)hipEventDestroy(c->dstreams.parts);
     delete c;
 }

@@ -1561,6 +1561,14 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     const uint32_t lzb = (n + 255) / 256;
     decomp_lane_kernel<3><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
                                               out_cap, d_out_descs, p.scount);
+    // the snappy lanes (second stream) start once the LZ4 lanes are done: both kernels'
+    // 1,024 workgroups want the whole GPU, and racing them for it slowed C3's LZ4 lanes
+    // (78 or 93 ms per step from run to run); in C5 the snappy lanes ran beside the zstd
+    // lanes, after the LZ4 lanes, anyway
+    if (ds) {
+        if ((e = hipEventRecord(ds->lanes, s)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(ws, ds->lanes, 0)) != hipSuccess) return e;
+    }
     // snappy lanes on the second stream after its wave decoders (C5: the main stream
     // carries the part kernels, the LZ4 lanes and the zstd lanes, the longer chain)
 #ifndef RPGPU_SNAPPY_LANE_AUX

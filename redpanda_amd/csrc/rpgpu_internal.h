@@ -53,6 +53,7 @@ struct Overlap {
 struct DecompStreams {
     hipStream_t aux, aux2;
     hipEvent_t fork, join, join2, parts;  // parts: the LZ4 part decoder (main stream) is done
+    hipEvent_t lanes;                     // the LZ4 lane decoder (main stream) is done
 };
 
 void build_tables(uint32_t* out /* kTableWords */);
