@@ -223,6 +223,7 @@ def full_check(spec, chunks, part_shift, res, dres, ores, index, gen_threads, pi
                 name = abi.VERDICT_NAMES.get(int(v), str(int(v)))
                 hist_o[name] = hist_o.get(name, 0) + int(n_)
             at += c
+            log(f"[full check] {at}/{len(res)} batches, {int(bad.sum())} mismatched so far")
     hist_g = {abi.VERDICT_NAMES.get(int(v), str(int(v))): int(n_)
               for v, n_ in zip(*np.unique(dres["verdict"], return_counts=True))}
     return {"batches": int(at), "mismatched_batches": int(bad.sum()), "mismatches_by_kind": kinds,
@@ -230,6 +231,20 @@ def full_check(spec, chunks, part_shift, res, dres, ores, index, gen_threads, pi
             "decompress_verdicts_gpu": hist_g, "decompress_verdicts_oracle": hist_o,
             "validation_verdicts_gpu": {abi.VERDICT_NAMES.get(int(v), str(int(v))): int(n_)
                                         for v, n_ in zip(*np.unique(res["verdict"], return_counts=True))}}
+
+
+def index_slices_equal(g_index, g_first, g_count, w_index, w_first, w_count) -> bool:
+    """Every batch's index entries equal, slice by slice (the two sides may lay
+    the slices out at different offsets)."""
+    if not np.array_equal(g_count, w_count):
+        return False
+    gi = g_index.view(np.uint8).reshape(-1, 32)
+    wi = w_index.view(np.uint8).reshape(-1, 32)
+    for j in np.nonzero(g_count)[0]:
+        a, b, m = int(g_first[j]), int(w_first[j]), int(g_count[j])
+        if a + m > len(gi) or b + m > len(wi) or not np.array_equal(gi[a:a + m], wi[b:b + m]):
+            return False
+    return True
 
 
 # ---- rank launcher (--gpus N without torchrun) -------------------------------------------
@@ -518,6 +533,11 @@ def main() -> int:
         if decompress:
             eng.decomp_plan_device(d_descs.data_ptr(), n, data.data_ptr(), d_res.data_ptr(),
                                    d_obytes.data_ptr(), d_dscr.data_ptr(), sh)
+            # the broker's flow: wait for the plan -- its output
+            # size and, in pinned memory, its per-decoder counts -- then run, so the
+            # run launches only the decoders the arena needs.
+            # The wait is inside the timed step.
+            stream.synchronize()
             eng.decomp_run_device(d_descs.data_ptr(), n, data.data_ptr(), d_res.data_ptr(),
                                   d_dres.data_ptr(), d_out.data_ptr(), out_cap, d_odescs.data_ptr(),
                                   d_ores.data_ptr(), d_index2.data_ptr(), max(rc_total, 1),
@@ -712,14 +732,27 @@ def main() -> int:
             same = same and (np.array_equal(dres["verdict"][n - sample_n:], tw["verdicts"])
                              and np.array_equal(dres["out_len"][n - sample_n:], tw["out_len"])
                              and all(np.array_equal(ores[f][n - sample_n:], tw["out_results"][f]) for f in names))
+            # the index entries of both samples too
+            gidx = d_index2.cpu().numpy().view(abi.INDEX_DTYPE)
+            for lo, ww in ((0, w), (n - sample_n, tw)):
+                sl = slice(lo, lo + sample_n)
+                same = same and index_slices_equal(gidx, ores["index_first"][sl], ores["index_count"][sl],
+                                                   ww["index"], ww["out_results"]["index_first"],
+                                                   ww["out_results"]["index_count"])
             what = ("the reference's wrapper loops over liblz4 1.9.3 / libzstd 1.4.9 / snappy 1.1.8 "
                     "+ decompress rewrite + record walk")
-            checked = f"first and last {sample_n} batches"
+            checked = f"first and last {sample_n} batches (results and index entries)"
         else:
-            ores_c = want[0]
+            ores_c, widx, _ = want
             same = all(np.array_equal(res[f][:sample_n], ores_c[f]) for f in names)
+            # and the sample's index entries
+            g_first, g_count = res["index_first"][:sample_n], res["index_count"][:sample_n]
+            end = int((g_first.astype(np.int64) + g_count).max(initial=0))
+            gidx = d_index[:end * 32].cpu().numpy().view(abi.INDEX_DTYPE)
+            same = same and index_slices_equal(gidx, g_first, g_count, widx, ores_c["index_first"],
+                                               ores_c["index_count"])
             what = "record walk + index"
-            checked = f"first {sample_n} batches"
+            checked = f"first {sample_n} batches (results and index entries)"
         orc.set_pin([])
         out["cpu_baseline"] = {
             "value": round(cpuT, 3), "unit": "GB/s", "cores": T, "kind": "port",

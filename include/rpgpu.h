@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RPGPU_ABI_VERSION 4
+#define RPGPU_ABI_VERSION 5
 #define RPGPU_ARENA_TAIL_PAD 64
 #define RPGPU_HEADER_SIZE 61 /* model/record.h:527-540 */
 
@@ -58,6 +58,11 @@ enum rpgpu_op {
      * them (reset_size_checksum_metadata, storage/parser_utils.cc:122-128);
      * used for the rewritten batches of rpgpu_decomp_run_device */
     RPGPU_OP_RECRC = 1u << 5,
+    /* LogAppendTime topics: rpgpu_set_max_timestamp_device re-stamps the
+     * batch (model::record_batch::set_max_timestamp, model/record.h:651-661,
+     * as produce_topic_partition calls it, kafka/server/handlers/produce.cc:
+     * 278-281); ignored by the validation kernels */
+    RPGPU_OP_APPEND_TIME = 1u << 6,
 };
 #define RPGPU_OPS_PRODUCE (RPGPU_OP_CRC | RPGPU_OP_HDRCRC | RPGPU_OP_PARSE | RPGPU_OP_INDEX)
 
@@ -336,6 +341,28 @@ int32_t rpgpu_run_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_descs, uint32
                          rpgpu_record_index* d_index, uint64_t index_cap,
                          const void* d_scratch, void* hip_stream);
 
+/* ---- append-time re-stamp (produce path) ---------------------------------
+ * model::record_batch::set_max_timestamp(ts_type, ts) (model/record.h:651-661)
+ * for every batch of a validated arena (d_results of rpgpu_validate_device /
+ * rpgpu_run_device over the same descriptors) whose descriptor has
+ * RPGPU_OP_APPEND_TIME and whose verdict is RPGPU_V_OK -- what
+ * produce_topic_partition does for a LogAppendTime topic with ts =
+ * model::timestamp::now() (kafka/server/handlers/produce.cc:278-281):
+ *   - timestamp type (attrs bit 3) already ts_type and max_timestamp == ts:
+ *     nothing changes (record.h:652-656);
+ *   - otherwise attrs bit 3 := ts_type, max_timestamp := ts, crc :=
+ *     crc_record_batch, header_crc := internal_header_only_crc: the batch's
+ *     bytes are rewritten in place (attrs, max_timestamp, crc; on-disk batches
+ *     also header_crc) and its result row takes the new attrs, max_timestamp,
+ *     crc, crc_expected and header_crc (the verdict stays OK).
+ * ts_type: 0 = create_time, 1 = append_time (model/timestamp.h).  The new crc
+ * is derived from the validated one without re-reading the body (CRC32C is
+ * affine: only the 22 bytes [21, 43) change).  d_changed (optional, one
+ * uint32 the caller zeroes) counts the batches that changed. */
+int32_t rpgpu_set_max_timestamp_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_descs, uint32_t n,
+                                       uint8_t* d_data, rpgpu_batch_result* d_results, int32_t ts_type,
+                                       int64_t ts, uint32_t* d_changed, void* hip_stream);
+
 /* ---- generic CRC32C over many byte ranges (device) ----------------------
  * crc_out[i] = crc32c::Extend(seed[i] (or 0), data + off[i], len[i]) —
  * the semantics of crc::crc32c::extend (hashing/crc32c.h:21-43). */
@@ -353,6 +380,12 @@ int32_t rpgpu_crc32c_extend(rpgpu_ctx* ctx, uint32_t crc, const void* p, size_t 
 int32_t rpgpu_internal_header_only_crc(rpgpu_ctx* ctx, const rpgpu_rp_header* h, uint32_t* out);
 int32_t rpgpu_crc_record_batch(rpgpu_ctx* ctx, const rpgpu_rp_header* h,
                                const void* body, size_t n, int32_t* out);
+/*   model::record_batch::set_max_timestamp  model/record.h:651-661
+ * on a header image and its records body: unchanged (RPGPU_OK, nothing
+ * written) when the timestamp type and max_timestamp already match, else
+ * attrs bit 3, max_timestamp, crc and header_crc updated in *h. */
+int32_t rpgpu_set_max_timestamp(rpgpu_ctx* ctx, rpgpu_rp_header* h, const void* body, size_t n,
+                                int32_t ts_type, int64_t ts);
 
 /* ---- decompression (storage read path) ---------------------------------
  * Replaces, per compressed batch,

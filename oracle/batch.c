@@ -464,3 +464,51 @@ uint64_t orc_index_total(const rpgpu_batch_desc* descs, uint32_t n, const uint8_
     for (uint32_t i = 0; i < n; i++) t += orc_index_cap(&descs[i], data);
     return t;
 }
+
+/* model::record_batch::set_max_timestamp (model/record.h:651-661) as
+ * produce_topic_partition applies it to accepted batches of LogAppendTime
+ * topics (kafka/server/handlers/produce.cc:278-281), per batch with
+ * RPGPU_OP_APPEND_TIME and verdict OK.  Both CRCs are recomputed from the
+ * whole rewritten batch, exactly as the reference does (crc_record_batch over
+ * the body, record_utils.cc:82-91; internal_header_only_crc, :34-55). */
+uint32_t orc_set_max_timestamp_arena(const rpgpu_batch_desc* descs, uint32_t n, uint8_t* data,
+                                     rpgpu_batch_result* res, int32_t ts_type, int64_t ts) {
+    uint32_t changed = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const rpgpu_batch_desc* d = &descs[i];
+        rpgpu_batch_result* r = &res[i];
+        if (!(d->ops & RPGPU_OP_APPEND_TIME) || (d->flags & RPGPU_DESC_NULL_RECORDS) || r->verdict != RPGPU_V_OK)
+            continue;
+        uint8_t* p = data + d->offset;
+        const int wire = d->format == RPGPU_FMT_KAFKA_WIRE;
+        rpgpu_rp_header h;
+        if (wire) {
+            rpgpu_batch_result tmp;
+            fill_from_wire_header(p, &tmp, &h);
+        } else {
+            memcpy(&h, p, sizeof(h));
+        }
+        if (((h.attrs >> 3) & 1) == ts_type && h.max_timestamp == ts) continue; /* record.h:652-656 */
+        h.attrs = (int16_t)(ts_type ? (h.attrs | 8) : (h.attrs & ~8)); /* record.h:307-309 */
+        h.max_timestamp = ts;
+        h.crc = orc_crc_record_batch(&h, p + RPGPU_HEADER_SIZE, (size_t)h.size_bytes - RPGPU_HEADER_SIZE);
+        h.header_crc = orc_internal_header_only_crc(&h);
+        if (wire) {
+            const uint16_t a = (uint16_t)h.attrs;
+            const uint64_t m = (uint64_t)h.max_timestamp;
+            const uint32_t c = (uint32_t)h.crc;
+            p[21] = (uint8_t)(a >> 8), p[22] = (uint8_t)a;
+            for (int k = 0; k < 8; k++) p[35 + k] = (uint8_t)(m >> (8 * (7 - k)));
+            for (int k = 0; k < 4; k++) p[17 + k] = (uint8_t)(c >> (8 * (3 - k)));
+        } else {
+            memcpy(p, &h, sizeof(h)); /* header_from_iobuf's little-endian image */
+        }
+        r->attrs = h.attrs;
+        r->max_timestamp = h.max_timestamp;
+        r->crc = (uint32_t)h.crc;
+        r->crc_expected = (uint32_t)h.crc;
+        r->header_crc = h.header_crc;
+        changed++;
+    }
+    return changed;
+}

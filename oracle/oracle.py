@@ -103,6 +103,8 @@ def lib() -> C.CDLL:
         L.orc_batch_timequery.argtypes = [vp, u32, vp, vp, u32, vp]
         L.orc_kafka_serialize.restype = None
         L.orc_kafka_serialize.argtypes = [vp, vp, vp, u32, vp, vp, u32, vp]
+        L.orc_set_max_timestamp_arena.restype = u32
+        L.orc_set_max_timestamp_arena.argtypes = [vp, u32, vp, vp, C.c_int32, C.c_int64]
         _L = L
     return _L
 
@@ -404,6 +406,18 @@ def compress_batches(data: np.ndarray, descs: np.ndarray, results: np.ndarray, c
         h["header_crc"] = internal_header_only_crc(h)
         out.append(h.tobytes() + payload)
     return out
+
+
+def set_max_timestamp_arena(data: np.ndarray, descs: np.ndarray, results: np.ndarray, ts: int,
+                            ts_type: int = 1) -> tuple[np.ndarray, np.ndarray, int]:
+    """record_batch::set_max_timestamp over an arena's accepted RPGPU_OP_APPEND_TIME
+    batches (produce.cc:278-281): (rewritten data, results, batches changed)."""
+    L = lib()
+    out = np.ascontiguousarray(data, dtype=np.uint8).copy()
+    descs = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+    res = np.ascontiguousarray(results, dtype=RESULT_DTYPE).copy()
+    ch = L.orc_set_max_timestamp_arena(descs.ctypes.data, len(descs), out.ctypes.data, res.ctypes.data, ts_type, ts)
+    return out, res, int(ch)
 
 
 def set_pin(cpus) -> None:

@@ -139,6 +139,12 @@ uint64_t orc_compact_rewrite(const uint8_t* data, const rpgpu_batch_desc* descs,
 void orc_batch_timequery(const rpgpu_batch_result* res, uint32_t n, const rpgpu_record_index* index,
                          const rpgpu_timequery* q, uint32_t nq, rpgpu_timequery_result* out);
 
+/* model::record_batch::set_max_timestamp (model/record.h:651-661) over the
+ * accepted batches with RPGPU_OP_APPEND_TIME (produce.cc:278-281): batch bytes
+ * and result rows updated in place; returns the batches changed. */
+uint32_t orc_set_max_timestamp_arena(const rpgpu_batch_desc* descs, uint32_t n, uint8_t* data,
+                                     rpgpu_batch_result* res, int32_t ts_type, int64_t ts);
+
 /* Fetch serialization (fetch.c): rpgpu_kafka_serialize_device restated. */
 void orc_kafka_serialize(const uint8_t* data, const rpgpu_batch_desc* descs, const int64_t* terms, uint32_t n,
                          uint8_t* out, const rpgpu_fetch_range* ranges, uint32_t nranges, rpgpu_fetch_summary* sums);

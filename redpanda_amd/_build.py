@@ -21,7 +21,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 LIBRPGPU = PKG / "librpgpu.so"
 LIBRPGEN = PKG / "librpgen.so"
 
-RPGPU_SRCS = ["rpgpu_kernels.hip", "rpgpu_decomp.hip", "rpgpu_sets.hip", "rpgpu_index.hip", "rpgpu_summary.hip", "rpgpu_compact.hip", "rpgpu_compact_rw.hip", "rpgpu_fetch.hip", "rpgpu_compress.hip", "rpgpu_abi.cpp", "rpgpu_tables.cpp"]
+RPGPU_SRCS = ["rpgpu_kernels.hip", "rpgpu_decomp.hip", "rpgpu_sets.hip", "rpgpu_index.hip", "rpgpu_summary.hip", "rpgpu_compact.hip", "rpgpu_compact_rw.hip", "rpgpu_fetch.hip", "rpgpu_compress.hip", "rpgpu_stamp.hip", "rpgpu_abi.cpp", "rpgpu_tables.cpp"]
 RPGPU_HDRS = ["rpgpu_internal.h", "rpgpu_device.h", "rpgpu_walk.h", "rpgpu_codec.h", "rpgpu_zstd.h", "rpgpu_zseq.h", "rpgpu_zblk.h", "rpgpu_wave.h", "rpgpu_inflate.h", "rpgpu_lz4c.h", "rpgpu_snappyc.h", "rpgpu_deflatec.h", "rpgpu_zstdc.h"]
 RPGEN_SRCS = ["rpgen.cpp"]
 RPGEN_HDRS = ["rpgen.h"]

@@ -28,6 +28,7 @@ OPT_ZSTD_SPLIT = 4  # RPGPU_OPT_ZSTD_SPLIT
 OPT_ZSTD_FUSED = 8  # RPGPU_OPT_ZSTD_FUSED
 OPT_ZSTD_WAVE_ONLY = 16  # RPGPU_OPT_ZSTD_WAVE_ONLY
 OP_RECRC = 32
+OP_APPEND_TIME = 64  # RPGPU_OP_APPEND_TIME (rpgpu_set_max_timestamp_device)
 OPS_PRODUCE = OP_CRC | OP_HDRCRC | OP_PARSE | OP_INDEX
 
 V_OK = 0
@@ -62,7 +63,7 @@ RPGPU_OK = 0
 RPGPU_PENDING = 1
 RPGPU_EINVAL = -1
 RPGPU_ECAPACITY = -4
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 DESC_NULL_RECORDS = 1  # rpgpu_batch_desc.flags
 
@@ -249,6 +250,9 @@ def lib() -> C.CDLL:
         _sig(L.rpgpu_compress_scratch_bytes, C.c_size_t, _u32)
         _sig(L.rpgpu_compress_plan_device, _i32, _vp, _vp, _u32, _i32, _vp, _vp, _vp)
         _sig(L.rpgpu_compress_run_device, _i32, _vp, _vp, _u32, _vp, _vp, _i32, _vp, _vp, _u64, _vp, _vp, _vp, _vp)
+        if hasattr(L, "rpgpu_set_max_timestamp"):  # ABI 5 (older builds: A/B timing runs)
+            _sig(L.rpgpu_set_max_timestamp, _i32, _vp, _vp, _vp, C.c_size_t, _i32, C.c_int64)
+            _sig(L.rpgpu_set_max_timestamp_device, _i32, _vp, _vp, _u32, _vp, _vp, _i32, C.c_int64, _vp, _vp)
         if not hasattr(L, "rpgpu_decomp_scratch_bytes"):  # an older build (A/B timing runs)
             _LIB = L
             return _LIB
@@ -300,4 +304,5 @@ EXPORTED = [
     "rpgpu_decomp_scratch_bytes", "rpgpu_decomp_scratch_bytes_ctx", "rpgpu_decomp_plan_device", "rpgpu_decomp_run_device",
     "rpgpu_uncompress", "rpgpu_decompress_batch", "rpgpu_record_sets_scratch_bytes", "rpgpu_record_sets_plan_device",
     "rpgpu_record_sets_run_device", "rpgpu_segment_index_device",
+    "rpgpu_set_max_timestamp", "rpgpu_set_max_timestamp_device",
 ]

@@ -100,6 +100,9 @@ hipError_t launch_compress_run(const rpgpu_batch_desc* d_descs, uint32_t n, cons
                                uint8_t* d_out, uint64_t out_cap, rpgpu_batch_desc* d_out_descs,
                                rpgpu_batch_result* d_vres2, void* d_scratch, const uint32_t* d_tables, int grid,
                                hipStream_t s);
+hipError_t launch_set_max_timestamp(const rpgpu_batch_desc* d_descs, uint32_t n, uint8_t* d_data,
+                                    rpgpu_batch_result* d_res, uint32_t ts_type, int64_t ts, uint32_t* d_changed,
+                                    hipStream_t s);
 hipError_t launch_kafka_serialize(const uint8_t* d_data, const rpgpu_batch_desc* d_descs, const int64_t* d_terms,
                                   uint32_t n, uint8_t* d_out, const rpgpu_fetch_range* d_ranges, uint32_t nranges,
                                   rpgpu_fetch_summary* d_sums, hipStream_t s);
@@ -443,6 +446,17 @@ int32_t rpgpu_kafka_error_codes_device(rpgpu_ctx* c, const rpgpu_batch_result* d
     return RPGPU_OK;
 }
 
+int32_t rpgpu_set_max_timestamp_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, uint32_t n, uint8_t* d_data,
+                                       rpgpu_batch_result* d_results, int32_t ts_type, int64_t ts,
+                                       uint32_t* d_changed, void* hip_stream) {
+    // model::timestamp_type: create_time 0, append_time 1 (model/timestamp.h)
+    if (!c || (n && (!d_descs || !d_data || !d_results)) || (ts_type != 0 && ts_type != 1)) return RPGPU_EINVAL;
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    hipError_t e = rpgpu::launch_set_max_timestamp(d_descs, n, d_data, d_results, (uint32_t)ts_type, ts, d_changed, s);
+    if (e != hipSuccess) return fail(c, e, "set_max_timestamp launch");
+    return RPGPU_OK;
+}
+
 const char* rpgpu_last_error(const rpgpu_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 int32_t rpgpu_device_info(const rpgpu_ctx* c, int32_t* cu_count, int32_t* grid) {
@@ -511,10 +525,12 @@ int32_t rpgpu_decomp_plan_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, 
                                  uint64_t* d_out_bytes, void* d_scratch, void* hip_stream) {
     if (!c || (n && (!d_descs || !d_data || !d_results || !d_scratch))) return RPGPU_EINVAL;
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->stream;
+    // forget the previous plan's counts first: a launch that fails part way may
+    // already have rewritten this scratch's counters
+    c->plan_scratch = nullptr;
     hipError_t e = rpgpu::launch_decomp_plan(d_descs, n, d_data, d_results, d_out_bytes, d_scratch,
                                               c->max_decoded, c->ws_lanes, c->zmode, s);
     if (e != hipSuccess) return fail(c, e, "decomp plan launch");
-    c->plan_scratch = nullptr;
     if (n && c->h_plan && c->plan_ev) {
         const uint8_t* cnt = static_cast<const uint8_t*>(d_scratch) + rpgpu::decomp_counter_offset(n, c->ws_lanes);
         if (hipMemcpyAsync(c->h_plan, cnt, 64 * sizeof(uint32_t), hipMemcpyDeviceToHost, s) == hipSuccess &&
@@ -901,6 +917,25 @@ int32_t rpgpu_internal_header_only_crc(rpgpu_ctx* c, const rpgpu_rp_header* h, u
     // are exactly the packed image's bytes [4, 61).
     if (!c || !h || !out) return RPGPU_EINVAL;
     return rpgpu_crc32c_extend(c, 0, reinterpret_cast<const uint8_t*>(h) + 4, RPGPU_HEADER_SIZE - 4, out);
+}
+
+int32_t rpgpu_set_max_timestamp(rpgpu_ctx* c, rpgpu_rp_header* h, const void* body, size_t n, int32_t ts_type,
+                                int64_t ts) {
+    // model::record_batch::set_max_timestamp (model/record.h:651-661), line for
+    // line, over the two scalar mirrors below
+    if (!c || !h || (n && !body) || (ts_type != 0 && ts_type != 1)) return RPGPU_EINVAL;
+    if (((h->attrs >> 3) & 1) == ts_type && h->max_timestamp == ts) return RPGPU_OK;
+    h->attrs = (int16_t)(ts_type ? (h->attrs | 8) : (h->attrs & ~8));  // record.h:307-309
+    h->max_timestamp = ts;
+    int32_t crc = 0;
+    int32_t st = rpgpu_crc_record_batch(c, h, body, n, &crc);
+    if (st != RPGPU_OK) return st;
+    h->crc = crc;
+    uint32_t hc = 0;
+    st = rpgpu_internal_header_only_crc(c, h, &hc);
+    if (st != RPGPU_OK) return st;
+    h->header_crc = hc;
+    return RPGPU_OK;
 }
 
 int32_t rpgpu_crc_record_batch(rpgpu_ctx* c, const rpgpu_rp_header* h, const void* body, size_t n, int32_t* out) {

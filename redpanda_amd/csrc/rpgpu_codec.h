@@ -497,7 +497,13 @@ RPC_HD void v16_st(uint8_t* p, const V16& x) {
     st16(p, v);
 }
 RPC_HD uint64_t funnel(uint64_t a, uint64_t b, uint32_t s) {  // bytes [s, s + 8) of a|b, s < 8
+#if defined(RPZS_NOP_SHIFT) && defined(__HIP_DEVICE_COMPILE__)  // diagnostics: wait states before the shifts
+    uint32_t r = 8 * s, l = 64 - 8 * s;
+    asm volatile("s_nop 4" : "+v"(r), "+v"(l));
+    return s ? (a >> r) | (b << l) : a;
+#else
     return s ? (a >> (8 * s)) | (b << (64 - 8 * s)) : a;
+#endif
 }
 // bytes [r, r + 16) of the 32 bytes x|y (bytes past 32 read as zero), r < 32
 RPC_HD V16 v16_ext(const V16& x, const V16& y, uint32_t r) {

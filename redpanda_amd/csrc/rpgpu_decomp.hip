@@ -912,8 +912,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_
 #endif
         const uint32_t i = zlist[k];
         const uint64_t off = block_base[i / kScanBlock] + local[i];
-        rpzstd::exec_lane(reinterpret_cast<const uint64_t*>(out + roff) + bs_r[k / kScanBlock] + recs[k],
-                          out + off + kHeaderSize);
+        RPZS_EXEC_CALL(reinterpret_cast<const uint64_t*>(out + roff) + bs_r[k / kScanBlock] + recs[k],
+                       out + off + kHeaderSize);
     }
 }
 

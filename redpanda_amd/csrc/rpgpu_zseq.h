@@ -475,6 +475,10 @@ RPC_HD uint64_t rw_next(RecWin& R) {
 // batches in 10^5, different ones run to run -- which the inlined form, the
 // exact-copy form and the host build never did (profiles/r5/NOTES.md r5h).
 RPC_HD void exec_lane(const uint64_t* rec, uint8_t* out) {
+#if defined(RPZS_EXEC_FLAT) && defined(__HIP_DEVICE_COMPILE__)  // diagnostics: flat accesses when inlined
+    asm volatile("" : "+v"(out));
+    asm volatile("" : "+v"(rec));
+#endif
     using rpcodec::V16;
     using rpcodec::v16_ld;
     using rpcodec::v16_st;
@@ -622,6 +626,34 @@ RPC_HD void exec_lane(const uint64_t* rec, uint8_t* out) {
         rpcodec::st_part(out + ca, cur.lo, cur.hi, (uint64_t)(op - ca));
     }
 }
+
+#if defined(RPZS_EXEC_NOINLINE) && defined(__HIP_DEVICE_COMPILE__)
+// diagnostics builds: exec_lane out of line, its pointers generic (flat
+// accesses) or, with RPZS_EXEC_GLOBAL, global ones (the call is all that differs
+// from the inlined form then)
+#ifdef RPZS_EXEC_GLOBAL
+__device__ __attribute__((noinline)) void exec_lane_ool(const __attribute__((address_space(1))) uint64_t* rec,
+                                                        __attribute__((address_space(1))) uint8_t* out) {
+    exec_lane((const uint64_t*)rec, (uint8_t*)out);
+}
+#define RPZS_EXEC_CALL(rec, out)                                                                  \
+    rpzstd::exec_lane_ool((const __attribute__((address_space(1))) uint64_t*)(rec), \
+                          (__attribute__((address_space(1))) uint8_t*)(out))
+#else
+__device__ __attribute__((noinline)) void exec_lane_ool(const uint64_t* rec, uint8_t* out) {
+#ifdef RPZS_NOP_EDGES  // diagnostics: wait states at the function's entry and exit
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+#endif
+    exec_lane(rec, out);
+#ifdef RPZS_NOP_EDGES
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+#endif
+}
+#define RPZS_EXEC_CALL(rec, out) rpzstd::exec_lane_ool((rec), (out))
+#endif
+#else
+#define RPZS_EXEC_CALL(rec, out) rpzstd::exec_lane((rec), (out))
+#endif
 
 }  // namespace rpzstd
 #endif

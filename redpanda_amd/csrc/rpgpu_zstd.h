@@ -236,6 +236,142 @@ RPC_HD void copy_seq_match(uint8_t* dst, uint64_t off, uint64_t n) {
     if (i < n) st_part(dst + i, lo, hi, n - i);
 }
 
+// ---------------------------------------------- write-combined sequences
+// The lane decoder's sequence execution (ZSTD_execSequence's copies, after its
+// checks) with the LZ4 lane decoder's register path (rpcodec::lz4_block_lane):
+// a sequence with <= 32 literal bytes and a match of <= 32 bytes whose source
+// lies before it (or any match with offset < 16: its period rebuilt in
+// registers) issues all its loads at once, composes the match bytes that come
+// from its own literals in registers, and appends sequences of <= 16 bytes to
+// a 32-byte register buffer (cur | cur1, output [ca, o)) that leaves as one
+// 32-byte store per 32 bytes filled.  Match sources still in the buffer are
+// overlaid from it.  So most sequences issue no store, and the next
+// sequence's FSE table loads do not wait behind stores (gfx9 counts loads and
+// stores in one vmcnt).  Longer sequences store their 16-byte chunks at once,
+// up to 15 bytes past their end (the next sequence overwrites them, the slot
+// has kSlack bytes after its capacity) -- unless that could reach literals
+// not consumed yet (Huffman / RLE literals sit in the slot tail right behind
+// the output, `lp`), where the exact copies above run instead.
+#ifndef RPGPU_ZSTD_WC
+#define RPGPU_ZSTD_WC 1
+#endif
+struct WcBuf {
+    rpcodec::V16 cur, cur1;
+    uint64_t ca;  // output below ca is in memory; [ca, o) in cur | cur1 (o - ca < 32)
+};
+RPC_HD void wc_flush(WcBuf& b, uint8_t* out, uint64_t o) {
+    const uint64_t f = o - b.ca;
+    if (f >= 16) {
+        rpcodec::v16_st(out + b.ca, b.cur);
+        if (f > 16) st_part(out + b.ca + 16, b.cur1.lo, b.cur1.hi, f - 16);
+    } else if (f) {
+        st_part(out + b.ca, b.cur.lo, b.cur.hi, f);
+    }
+    b.ca = o;
+}
+// literals lp[0, ll) at out + o, then a match of ml bytes at distance off
+// (checked: within the output, the literals present)
+RPC_HD void wc_seq(WcBuf& b, uint8_t* out, uint64_t o, const uint8_t* lp, uint64_t ll, uint64_t ml, uint64_t off) {
+    using rpcodec::V16;
+    using rpcodec::v16_ext;
+    using rpcodec::v16_merge;
+    using rpcodec::v16_overlay;
+    using rpcodec::v16_shl;
+    using rpcodec::v16_st;
+    const uint64_t op_m = o + ll, end = op_m + ml;
+    const bool pat = off < 16;
+    const uint64_t nch = pat ? 1 : (ml + 15) >> 4;
+    // stores reach at most end + 15: keep them below the literals still to come
+    const uintptr_t lnext = (uintptr_t)(lp + ll);
+    const bool room = lnext >= (uintptr_t)(out + end + 16) || lnext < (uintptr_t)out;
+    if (ll > 32 || (!pat && (ml > 32 || off < 16 * nch)) || !room) {
+        wc_flush(b, out, o);
+        copy_lits(out + o, lp, ll);
+        copy_seq_match(out + op_m, off, ml);
+        b.ca = end;
+        return;
+    }
+    // one round trip: every load of the sequence, then its stores
+    const int64_t rel = (int64_t)ll - (int64_t)off;  // match source start - literal start
+    const uint8_t* src = out + op_m - off;
+    V16 L0{0, 0}, L1{0, 0}, A0{0, 0}, A1{0, 0};
+    if (ll > 0) L0 = rpcodec::v16_ld(lp);
+    if (ll > 16) L1 = rpcodec::v16_ld(lp + 16);
+    if (rel < 0) A0 = rpcodec::v16_ld(src);
+    if (!pat && nch > 1 && rel + 16 < 0) A1 = rpcodec::v16_ld(src + 16);
+    if (o > b.ca && rel < 0) {
+        // source bytes in [ca, o) are still in cur | cur1 (32-bit positions:
+        // a frame's output is below 2^31 here, the slot ceiling)
+        const int32_t sb = (int32_t)(op_m - off), ca = (int32_t)b.ca;
+        A0 = v16_overlay(v16_overlay(A0, sb, b.cur, ca), sb, b.cur1, ca + 16);
+        if (!pat && nch > 1 && rel + 16 < 0)
+            A1 = v16_overlay(v16_overlay(A1, sb + 16, b.cur, ca), sb + 16, b.cur1, ca + 16);
+    }
+    // 16 source bytes at literal-relative r: stored bytes (A) below the
+    // literal run, the run's own bytes (registers) from it on
+    const int64_t r0 = rel, r1 = rel + 16;
+    const V16 c0 = r0 >= 0 ? v16_ext(L0, L1, (uint32_t)r0)
+                   : r0 <= -16 ? A0 : v16_merge(A0, v16_shl(L0, (uint32_t)-r0), (uint32_t)-r0);
+    V16 first = c0;
+    uint64_t step = 16;
+    if (pat) {
+        uint64_t lo = c0.lo, hi = c0.hi;
+        if (off <= 8) {
+            if (off < 8) lo &= (1ull << (8 * off)) - 1;
+            hi = 0;
+        } else {
+            hi &= (1ull << (8 * (off - 8))) - 1;
+        }
+        for (uint64_t w = off; w < 16; w *= 2) {
+            const uint64_t sh = 8 * w;
+            if (sh < 64) {
+                hi |= (hi << sh) | (lo >> (64 - sh));
+                lo |= lo << sh;
+            } else {
+                hi |= lo << (sh - 64);
+            }
+        }
+        step = off * (16 / off);
+        first = V16{lo, hi};
+    }
+    if (ll + ml <= 16) {
+        // the whole sequence in one 16-byte piece, appended to `cur`
+        const V16 sq = ll ? v16_merge(L0, v16_shl(first, (uint32_t)ll), (uint32_t)ll) : first;
+        const uint32_t f = (uint32_t)(o - b.ca);
+        if (f < 16) {
+            b.cur = f ? v16_merge(b.cur, v16_shl(sq, f), f) : sq;
+            b.cur1 = v16_ext(sq, V16{0, 0}, 16 - f);
+        } else {
+            const uint32_t g = f - 16;
+            const V16 c1 = g ? v16_merge(b.cur1, v16_shl(sq, g), g) : sq;
+            if (f + (uint32_t)(ll + ml) >= 32) {
+                v16_st(out + b.ca, b.cur);
+                v16_st(out + b.ca + 16, c1);
+                b.cur = v16_ext(sq, V16{0, 0}, 16 - g);
+                b.ca += 32;
+            } else {
+                b.cur1 = c1;
+            }
+        }
+        return;
+    }
+    if (o > b.ca) v16_st(out + b.ca, b.cur);  // wild: the stores below overwrite [o, ca + 32)
+    if (o > b.ca + 16) v16_st(out + b.ca + 16, b.cur1);
+    b.ca = end;
+    if (ll > 0) v16_st(out + o, L0);
+    if (ll > 16) v16_st(out + o + 16, L1);
+    if (pat) {
+        for (uint64_t i = 0; i < ml; i += step) v16_st(out + op_m + i, first);
+    } else {
+        v16_st(out + op_m, c0);
+        if (nch > 1) {
+            const V16 c1 = r1 >= 0 ? v16_ext(L0, L1, (uint32_t)r1)
+                           : r1 <= -16 ? A1 : v16_merge(A1, v16_shl(L0, (uint32_t)-r1), (uint32_t)-r1);
+            v16_st(out + op_m + 16, c1);
+        }
+    }
+}
+
 RPC_HD void fill_bytes(uint8_t* dst, uint8_t v, uint64_t n) {
     const uint64_t x = 0x0101010101010101ull * v;
     rpcodec::B16 p;
@@ -776,6 +912,11 @@ struct Huf4 {
 RPC_HD uint64_t xxh64(const uint8_t* p, uint64_t len);
 struct DirectEmit {
     static constexpr bool kInlineBlocks = false;
+#if RPGPU_ZSTD_WC && !defined(RPGPU_DIAG_NOCOPY)
+    static constexpr bool kWc = true;  // block()'s sequences write-combined (wc_seq)
+#else
+    static constexpr bool kWc = false;
+#endif
     // hooks of the split decoder (rpgpu_zseq.h): a literals section begins, its
     // Huffman table is read, a frame checksum is checked over the decoded bytes
     RPC_HD void section_begin() {}
@@ -829,6 +970,16 @@ struct DirectEmit {
         return h0.ok && h1.ok && h2.ok && h3.ok;
     }
 #endif
+};
+
+// E::kWc where the emitter declares it (DirectEmit), else false
+template <class E, class = void>
+struct wc_of {
+    static constexpr bool value = false;
+};
+template <class E>
+struct wc_of<E, decltype((void)E::kWc)> {
+    static constexpr bool value = E::kWc;
 };
 
 // ---------------------------------------------------------------- blocks
@@ -1237,6 +1388,10 @@ RPZ_COLD int64_t block(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out,
     const uint8_t* const lend = lit.p + lit.n;
     uint64_t o = op;
     if (nbSeq) {
+        // the lane decoders' sequences go through the write-combined path (wc_seq)
+        constexpr bool kWc = !kRing && wc_of<E>::value;
+        WcBuf wc{};
+        wc.ca = o;
         w.fse_entropy = 1;
         Bits b;
         if (!bits_init(b, p, (uint64_t)(iend - p))) return RPZ_FAIL(-1);
@@ -1305,11 +1460,16 @@ RPZ_COLD int64_t block(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out,
                     continue;
                 }
             }
-            em.lits(out + o, lp, ll);
+            if constexpr (kWc) {
+                wc_seq(wc, out, o, lp, ll, ml, offset);
+            } else {
+                em.lits(out + o, lp, ll);
+                em.match(out + lit_end, offset, ml);
+            }
             lp += ll;
-            em.match(out + lit_end, offset, ml);
             o = lit_end + ml;
         }
+        if constexpr (kWc) wc_flush(wc, out, o);
 #if RPZ_PROF
         w.t_seq += RPZ_CLK() - c1;
         w.n_seq += nbSeq;

@@ -598,6 +598,55 @@ class Engine:
             raise EngineError(f"rpgpu_crc_record_batch: {rc} {self.last_error()}")
         return int(out.value)
 
+    def set_max_timestamp(self, hdr: np.ndarray, body: bytes | np.ndarray, ts_type: int, ts: int) -> np.ndarray:
+        """model::record_batch::set_max_timestamp (model/record.h:651-661) on a
+        header image and its records body (rpgpu_set_max_timestamp); returns the
+        updated header."""
+        h = np.ascontiguousarray(hdr, dtype=abi.RP_HEADER_DTYPE).reshape(1).copy()
+        b = np.ascontiguousarray(np.frombuffer(bytes(body), dtype=np.uint8))
+        rc = self._lib.rpgpu_set_max_timestamp(self._ctx, h.ctypes.data, b.ctypes.data if b.size else None,
+                                               b.size, ts_type, ts)
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_set_max_timestamp: {rc} {self.last_error()}")
+        return h[0]
+
+    def set_max_timestamp_device(self, d_descs: int, n: int, d_data: int, d_results: int, ts_type: int, ts: int,
+                                 d_changed: int = 0, stream: int = 0) -> None:
+        rc = self._lib.rpgpu_set_max_timestamp_device(self._ctx, d_descs, n, d_data, d_results, ts_type, ts,
+                                                      d_changed or None, _stream(stream))
+        if rc != abi.RPGPU_OK:
+            raise EngineError(f"rpgpu_set_max_timestamp_device: {rc} {self.last_error()}")
+
+    def append_time_arena(self, data: np.ndarray, descs: np.ndarray, ts: int, ts_type: int = 1) -> dict:
+        """The produce path of a LogAppendTime topic over a host arena: validate
+        (rpgpu_validate_device), then re-stamp the accepted batches whose
+        descriptors carry RPGPU_OP_APPEND_TIME (rpgpu_set_max_timestamp_device).
+        Returns host copies: results (after the re-stamp), data (the arena with
+        the rewritten headers), changed (batches re-stamped)."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        descs = np.ascontiguousarray(descs, dtype=abi.DESC_DTYPE)
+        n = len(descs)
+        m = max(n, 1)
+        sh = torch.cuda.current_stream(dev).cuda_stream
+        d_data = torch.from_numpy(data.copy()).to(dev)
+        d_descs = torch.from_numpy(descs.view(np.uint8).copy()).to(dev)
+        d_res = torch.zeros(m * 64, dtype=torch.uint8, device=dev)
+        d_used = torch.zeros(1, dtype=torch.int64, device=dev)
+        d_scr = torch.zeros(max(self.scratch_bytes(n), 1), dtype=torch.uint8, device=dev)
+        index_cap = int(descs["length"].astype(np.uint64).sum() // 2) + 1
+        d_index = torch.zeros(index_cap * 32, dtype=torch.uint8, device=dev)
+        d_changed = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.validate_device(d_descs.data_ptr(), n, d_data.data_ptr(), d_res.data_ptr(), d_index.data_ptr(),
+                             index_cap, d_used.data_ptr(), d_scr.data_ptr(), sh)
+        self.set_max_timestamp_device(d_descs.data_ptr(), n, d_data.data_ptr(), d_res.data_ptr(), ts_type, ts,
+                                      d_changed.data_ptr(), sh)
+        torch.cuda.synchronize(dev)
+        return dict(results=d_res.cpu().numpy().view(abi.RESULT_DTYPE)[:n].copy(), data=d_data.cpu().numpy(),
+                    changed=int(d_changed.item()))
+
     # -- produce-handler glue -----------------------------------------------------------
     def eventfd(self) -> int:
         return int(self._lib.rpgpu_eventfd(self._ctx))
