@@ -399,9 +399,8 @@ def main() -> int:
                     help="the record walk beside the checksums (auto: the library default, on; "
                          "off: RPGPU_OPT_NO_WALK_OVERLAP)")
     ap.add_argument("--blocks-per-cu", type=int, default=0, help="rpgpu_opts.blocks_per_cu (tuning; 0 = default)")
-    ap.add_argument("--zstd-split", default="off", choices=["off", "lds", "fused"],
-                    help="zstd lane bodies through the split decoder (lds: RPGPU_OPT_ZSTD_SPLIT, fused: "
-                         "RPGPU_OPT_ZSTD_FUSED; A/B measurements)")
+    ap.add_argument("--ws-lanes", type=int, default=0,
+                    help="rpgpu_opts.decomp_ws_lanes: zstd lane decoders in flight (tuning; 0 = default)")
     ap.add_argument("--zstd-blocks", default="on", choices=["on", "off"],
                     help="large zstd frames block-parallel (on, the default) or on the wave decoder only "
                          "(off: RPGPU_OPT_ZSTD_WAVE_ONLY; A/B measurements)")
@@ -443,8 +442,8 @@ def main() -> int:
     # the chunked checksum / walk overlap is the library's default (C3 / C4 / C5 within 1 %
     # of serial validate-then-walk, C2 ~9 % faster; profiles/r4/NOTES.md r4i / r4j)
     overlap = args.overlap != "off"
-    eng = engine.Engine(local, walk_overlap=overlap, decomp_ws_lanes=cfg.get("ws_lanes", 0),
-                        walk_chunks=args.walk_chunks, blocks_per_cu=args.blocks_per_cu, zstd_split=False if args.zstd_split == "off" else args.zstd_split,
+    eng = engine.Engine(local, walk_overlap=overlap, decomp_ws_lanes=args.ws_lanes or cfg.get("ws_lanes", 0),
+                        walk_chunks=args.walk_chunks, blocks_per_cu=args.blocks_per_cu,
                         zstd_blocks=args.zstd_blocks == "on")
     chunks, P_total, part_shift, (plo, phi) = rank_chunks(cfg, rank, world, scaling, args.batches)
     n = sum(m for _, m in chunks)
@@ -641,9 +640,15 @@ def main() -> int:
         try:
             key = args.config if (not decompress or args.payload == "text") else f"{args.config}:{args.payload}"
             tr = json.load(open(prof)).get(key)
+            # only PMC passes of this exact library count
+            lib_hash = engine.library_hash()
             if tr and tr.get("batches") == n and tr.get("payload", "text") == (args.payload if decompress else "text"):
-                out["roofline"]["traffic"] = tr.get("hbm_bytes_per_launch")
-                out["roofline"]["traffic_source"] = f"profiles/traffic.json[{key!r}]"
+                if tr.get("lib_sha256_16") == lib_hash:
+                    out["roofline"]["traffic"] = tr.get("hbm_bytes_per_launch")
+                    out["roofline"]["traffic_source"] = f"profiles/traffic.json[{key!r}]"
+                else:
+                    out["roofline"]["traffic_note"] = (f"profiles/traffic.json[{key!r}] was measured on library "
+                                                       f"{tr.get('lib_sha256_16')}, not this one ({lib_hash})")
         except (OSError, ValueError):
             pass
 

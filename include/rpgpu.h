@@ -200,14 +200,11 @@ typedef struct rpgpu_rp_header {
  * RPGPU_OPT_NO_WALK_OVERLAP checksums the whole arena, then walks it. */
 #define RPGPU_OPT_WALK_OVERLAP 1u
 #define RPGPU_OPT_NO_WALK_OVERLAP 2u
-/* RPGPU_OPT_ZSTD_SPLIT: zstd bodies of lane-sized batches go through the
- * split decoder (entropy stages with their tables in LDS, then the sequences
- * executed; rpgpu_zseq.h) instead of the one-lane decoder (tables in HBM).
- * Same verdicts and bytes; off by default (slower on C4 so far). */
+/* RPGPU_OPT_ZSTD_SPLIT / RPGPU_OPT_ZSTD_FUSED (ABI 4): the split zstd decoder
+ * for lane-sized frames, measured slower than the one-lane decoder and removed
+ * in ABI 5; the flags are accepted and ignored (every lane-sized zstd frame
+ * takes the one-lane decoder, whose sequences are write-combined since ABI 5). */
 #define RPGPU_OPT_ZSTD_SPLIT 4u
-/* RPGPU_OPT_ZSTD_FUSED: the one-lane decoder's entropy stages (tables in HBM)
- * writing copy records, then the split decoder's executor (rpgpu_zseq.h
- * RecEmit + exec_lane).  Same verdicts and bytes. */
 #define RPGPU_OPT_ZSTD_FUSED 8u
 /* RPGPU_OPT_ZSTD_WAVE_ONLY: zstd frames above the lane decoders' slots all go
  * to the one-wave-per-frame decoder.  By default a large frame that is one

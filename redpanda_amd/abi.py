@@ -24,8 +24,8 @@ OP_INDEX = 8
 OP_DECOMP = 16
 OPT_WALK_OVERLAP = 1  # rpgpu_opts.flags: RPGPU_OPT_WALK_OVERLAP (the default)
 OPT_NO_WALK_OVERLAP = 2  # RPGPU_OPT_NO_WALK_OVERLAP
-OPT_ZSTD_SPLIT = 4  # RPGPU_OPT_ZSTD_SPLIT
-OPT_ZSTD_FUSED = 8  # RPGPU_OPT_ZSTD_FUSED
+OPT_ZSTD_SPLIT = 4  # RPGPU_OPT_ZSTD_SPLIT (ignored since ABI 5)
+OPT_ZSTD_FUSED = 8  # RPGPU_OPT_ZSTD_FUSED (ignored since ABI 5)
 OPT_ZSTD_WAVE_ONLY = 16  # RPGPU_OPT_ZSTD_WAVE_ONLY
 OP_RECRC = 32
 OP_APPEND_TIME = 64  # RPGPU_OP_APPEND_TIME (rpgpu_set_max_timestamp_device)

@@ -163,7 +163,7 @@ struct rpgpu_ctx {
     bool busy = false;  // one in-flight submission per context (shard-owned)
     uint64_t max_decoded = RPGPU_DEFAULT_MAX_DECODED_BATCH;  // opts.max_decoded_batch
     uint32_t ws_lanes = 0;  // opts.decomp_ws_lanes (0: the default ceiling)
-    uint32_t zmode = 0;     // zstd lane bodies: 0 one-lane, 1 split (LDS), 2 fused + executor
+    uint32_t zmode = 0;     // bit 2: large zstd frames on the wave decoder only (RPGPU_OPT_ZSTD_WAVE_ONLY)
     // the last decompress plan's queue counters, copied to the host behind it: a run
     // of that plan (same scratch and n) whose copy has landed skips launches with no work
     uint32_t* h_plan = nullptr;  // pinned, 64 words
@@ -258,8 +258,8 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
     // the walk of chunk k beside the checksums of chunk k + 1:
     // on unless RPGPU_OPT_NO_WALK_OVERLAP
     const bool want_overlap = !(opts && (opts->flags & RPGPU_OPT_NO_WALK_OVERLAP));
-    c->zmode = !opts ? 0u : (opts->flags & RPGPU_OPT_ZSTD_SPLIT) ? 1u : (opts->flags & RPGPU_OPT_ZSTD_FUSED) ? 2u : 0u;
-    if (opts && (opts->flags & RPGPU_OPT_ZSTD_WAVE_ONLY)) c->zmode |= 4u;  // kZModeNoBlk
+    // RPGPU_OPT_ZSTD_SPLIT / _FUSED are accepted and ignored since ABI 5 (rpgpu.h)
+    c->zmode = (opts && (opts->flags & RPGPU_OPT_ZSTD_WAVE_ONLY)) ? 4u : 0u;  // kZModeNoBlk
     if (!want_overlap) c->have_overlap = false;
     if (hipHostMalloc(reinterpret_cast<void**>(&c->h_plan), 64 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
         hipEventCreateWithFlags(&c->plan_ev, hipEventDisableTiming) != hipSuccess) {

@@ -497,13 +497,7 @@ RPC_HD void v16_st(uint8_t* p, const V16& x) {
     st16(p, v);
 }
 RPC_HD uint64_t funnel(uint64_t a, uint64_t b, uint32_t s) {  // bytes [s, s + 8) of a|b, s < 8
-#if defined(RPZS_NOP_SHIFT) && defined(__HIP_DEVICE_COMPILE__)  // diagnostics: wait states before the shifts
-    uint32_t r = 8 * s, l = 64 - 8 * s;
-    asm volatile("s_nop 4" : "+v"(r), "+v"(l));
-    return s ? (a >> r) | (b << l) : a;
-#else
     return s ? (a >> (8 * s)) | (b << (64 - 8 * s)) : a;
-#endif
 }
 // bytes [r, r + 16) of the 32 bytes x|y (bytes past 32 read as zero), r < 32
 RPC_HD V16 v16_ext(const V16& x, const V16& y, uint32_t r) {
@@ -1115,192 +1109,6 @@ RPC_HD bool snappy_raw(E& em, const uint8_t* in, uint64_t n, uint8_t* out, uint3
     }
 }
 
-// snappy_raw in the LZ4 lane decoder's form (lz4_block_lane): tags, lengths
-// and offsets from a 64-byte register window with the next 32 bytes in
-// flight, a literal element and the copy after it executed as one sequence
-// with all its loads issued at once, output write-combined in 32-byte register
-// buffers; runs of more than 32 literal bytes or copies whose 16-byte chunks
-// would read bytes they write take exact copies, and so does everything within
-// 16 bytes of `expected` (a split chunk's output ends there: the next chunk's
-// follows).  Acceptance is snappy_raw's, check for check.  `lim` = bytes of
-// `in` that may be read.  Host-compiled by tests/native/codec_fuzz.cpp.
-// Opt-in (RPGPU_SNAPPY_LANE=1): measured slower than snappy_raw on C5 (parts
-// 102 vs 65 ms, lanes 39 vs 18 ms: snappy's elements are shorter than LZ4's
-// sequences and the fused form's selects cost more than the loads they save).
-// Inlined: out of line (flat pointers) its loads of bytes it had just stored
-// came back stale on the device (a C5 snappy-java body's parts; round 5's
-// split zstd executor showed the same, profiles/r5/NOTES.md r5c-r5i).
-#ifndef RPGPU_SNAPPY_LANE
-#define RPGPU_SNAPPY_LANE 0
-#endif
-RPC_HD bool snappy_raw_lane(const uint8_t* in, int32_t n, uint8_t* out, int32_t expected, int32_t hdr, int32_t lim) {
-    int32_t ip = hdr, op = 0;
-    const int32_t oend = expected;
-    Win64 W;
-    w64_load(W, in, ip, lim);
-    V16 cur{0, 0}, cur1{0, 0};  // output [ca, op), not stored yet (op - ca < 32)
-    int32_t ca = 0;
-    int32_t ll = 0, ip_lit = ip;  // a literal element waiting for the copy after it
-    for (;;) {
-        int32_t ml = 0, off = 0;
-        bool last = false;
-        if (ip == n) {
-            last = true;  // eof at a tag boundary
-        } else {
-            if (ip >= W.pos + 32) {
-                if (ip < W.pos + 64 && W.npos == W.pos + 64) w64_shift(W, in, lim);
-                else w64_load(W, in, ip, lim);
-            }
-            const uint32_t c = w64_at(W, in, ip, 1, lim) & 255u;
-            const uint32_t type = c & 3u;
-            const int32_t extra = type == 0 ? ((c >> 2) >= 60 ? (int32_t)(c >> 2) - 59 : 0) : (type == 3 ? 4 : (int32_t)type);
-            if (n - ip < extra + 1) return false;
-            ip++;
-            const uint32_t x = extra ? w64_at(W, in, ip, extra, lim) : 0u;
-            if (type == 0) {
-                uint32_t len = (c >> 2) + 1;
-                if (len >= 61) {
-                    const uint32_t v = extra == 4 ? x : x & ((1u << (8 * extra)) - 1);
-                    len = v + 1;  // uint32 arithmetic, as ExtractLowBytes(...) + 1
-                    ip += extra;
-                }
-                if ((uint32_t)(n - ip) < len) return false;                      // premature end of input
-                if ((uint64_t)op + (uint64_t)ll + len > (uint64_t)expected) return false;  // SnappyArrayWriter::Append
-                if (ll == 0) {
-                    ll = (int32_t)len;
-                    ip_lit = ip;
-                    ip += (int32_t)len;
-                    continue;  // the copy after it joins this sequence
-                }
-                // a second literal element in a row (rare): the first goes out
-                // alone, exactly, and this one waits for its copy
-                if (op - ca >= 16) {
-                    v16_st(out + ca, cur);
-                    if (op - ca > 16) st_part(out + ca + 16, cur1.lo, cur1.hi, (uint64_t)(op - ca - 16));
-                } else if (op > ca) {
-                    st_part(out + ca, cur.lo, cur.hi, (uint64_t)(op - ca));
-                }
-                copy_exact(out + op, in + ip_lit, (uint64_t)ll);
-                op += ll;
-                ca = op;
-                ll = (int32_t)len;
-                ip_lit = ip;
-                ip += (int32_t)len;
-                continue;
-            } else {
-                if (type == 1) {
-                    ml = 4 + (int32_t)((c >> 2) & 7u);
-                    off = (int32_t)(((c >> 5) << 8) | (x & 255u));
-                } else if (type == 2) {
-                    ml = (int32_t)(c >> 2) + 1;
-                    off = (int32_t)(x & 0xFFFFu);
-                } else {
-                    ml = (int32_t)(c >> 2) + 1;
-                    if (x > 0x7FFFFFFFu) return false;  // beyond any output (Produced() <= offset - 1u)
-                    off = (int32_t)x;
-                }
-                ip += extra;
-                const int32_t opm = op + ll;
-                if (off == 0 || opm < off) return false;  // Produced() <= offset - 1u
-                if ((int64_t)opm + ml > (int64_t)expected) return false;
-            }
-        }
-        const int32_t op_m = op + ll;
-        // ---- copies (lz4_block_lane's)
-        const bool pat = off < 16;
-        const int32_t nch = pat ? 1 : (ml + 15) >> 4;
-        if (last || ll > 32 || (!pat && (ml > 32 || off < 16 * nch)) || op_m + ml + 15 > oend) {
-            if (op - ca >= 16) {
-                v16_st(out + ca, cur);
-                if (op - ca > 16) st_part(out + ca + 16, cur1.lo, cur1.hi, (uint64_t)(op - ca - 16));
-            } else if (op > ca) {
-                st_part(out + ca, cur.lo, cur.hi, (uint64_t)(op - ca));
-            }
-            if (ll) copy_exact(out + op, in + ip_lit, (uint64_t)ll);
-            if (last) return op + ll == expected;  // CheckLength
-            match_exact(out + op_m, (uint64_t)off, (uint64_t)ml);
-            op = op_m + ml;
-            ca = op;
-            ll = 0;
-            continue;
-        }
-        const int32_t rel = ll - off;
-        const uint8_t* src = out + op_m - off;
-        V16 L0{0, 0}, L1{0, 0}, A0{0, 0}, A1{0, 0};
-        if (ll > 0) L0 = lit16(W, in, ip_lit);
-        if (ll > 16) L1 = lit16(W, in, ip_lit + 16);
-        if (rel < 0) A0 = v16_ld(src);
-        if (!pat && nch > 1 && rel + 16 < 0) A1 = v16_ld(src + 16);
-        if (op > ca && rel < 0) {
-            const int32_t sb = op_m - off;
-            A0 = v16_overlay(v16_overlay(A0, sb, cur, ca), sb, cur1, ca + 16);
-            if (!pat && nch > 1 && rel + 16 < 0)
-                A1 = v16_overlay(v16_overlay(A1, sb + 16, cur, ca), sb + 16, cur1, ca + 16);
-        }
-        const int32_t r0 = rel, r1 = rel + 16;
-        const V16 c0 = r0 >= 0 ? v16_ext(L0, L1, (uint32_t)r0)
-                       : r0 <= -16 ? A0 : v16_merge(A0, v16_shl(L0, (uint32_t)-r0), (uint32_t)-r0);
-        V16 first = c0;
-        uint64_t step = 16;
-        if (pat) {
-            uint64_t lo = c0.lo, hi = c0.hi;
-            if (off <= 8) {
-                if (off < 8) lo &= (1ull << (8 * off)) - 1;
-                hi = 0;
-            } else {
-                hi &= (1ull << (8 * (off - 8))) - 1;
-            }
-            for (uint64_t w = (uint64_t)off; w < 16; w *= 2) {
-                const uint64_t sh = 8 * w;
-                if (sh < 64) {
-                    hi |= (hi << sh) | (lo >> (64 - sh));
-                    lo |= lo << sh;
-                } else {
-                    hi |= lo << (sh - 64);
-                }
-            }
-            step = (uint64_t)off * (16 / (uint64_t)off);
-            first = V16{lo, hi};
-        }
-        if (ll + ml <= 16) {
-            const V16 sq = ll ? v16_merge(L0, v16_shl(first, (uint32_t)ll), (uint32_t)ll) : first;
-            const uint32_t f = (uint32_t)(op - ca);
-            if (f < 16) {
-                cur = f ? v16_merge(cur, v16_shl(sq, f), f) : sq;
-                cur1 = v16_ext(sq, V16{0, 0}, 16 - f);
-            } else {
-                const uint32_t g = f - 16;
-                const V16 c1 = g ? v16_merge(cur1, v16_shl(sq, g), g) : sq;
-                if (f + (uint32_t)(ll + ml) >= 32) {
-                    v16_st(out + ca, cur);
-                    v16_st(out + ca + 16, c1);
-                    cur = v16_ext(sq, V16{0, 0}, 16 - g);
-                    ca += 32;
-                } else {
-                    cur1 = c1;
-                }
-            }
-        } else {
-            if (op > ca) v16_st(out + ca, cur);
-            if (op > ca + 16) v16_st(out + ca + 16, cur1);
-            ca = op_m + ml;
-            if (ll > 0) v16_st(out + op, L0);
-            if (ll > 16) v16_st(out + op + 16, L1);
-            if (pat) {
-                for (uint64_t i = 0; i < (uint64_t)ml; i += step) v16_st(out + op_m + i, first);
-            } else {
-                v16_st(out + op_m, c0);
-                if (nch > 1) {
-                    const V16 c1 = r1 >= 0 ? v16_ext(L0, L1, (uint32_t)r1)
-                                   : r1 <= -16 ? A1 : v16_merge(A1, v16_shl(L0, (uint32_t)-r1), (uint32_t)-r1);
-                    v16_st(out + op_m + 16, c1);
-                }
-            }
-        }
-        op = op_m + ml;
-        ll = 0;
-    }
-}
 
 // snappy_standard_compressor::uncompress_append via the C API as the oracle
 // calls it (oracle/codec.c snappy_raw_append): the length preamble, then a
@@ -1313,13 +1121,7 @@ RPC_HD int32_t snappy_raw_append(E& em, const uint8_t* in, uint64_t n, uint8_t* 
     if (!snappy_varint(in, n, ulen, used)) return V_ERROR;
     if (zero_skip && ulen == 0) return V_OK;
     if (o + ulen > cap) return V_OVERFLOW;
-    if constexpr (IsLane<E>::value && RPGPU_SNAPPY_LANE) {
-        // the input is readable kInPad bytes past the chunk (the next chunk, the arena's pad)
-        if (!snappy_raw_lane(in, (int32_t)n, out + o, (int32_t)ulen, (int32_t)used, (int32_t)(n + kInPad)))
-            return V_ERROR;
-    } else {
-        if (!snappy_raw(em, in, n, out + o, ulen, used)) return V_ERROR;
-    }
+    if (!snappy_raw(em, in, n, out + o, ulen, used)) return V_ERROR;
     o += ulen;
     return V_OK;
 }
@@ -1451,14 +1253,8 @@ RPC_HD int64_t decode_part(uint32_t kind, const uint8_t* in, uint64_t in_len, ui
         copy_exact(out, in, in_len);
         return (int64_t)in_len;
     }
-#if RPGPU_SNAPPY_LANE
-    return snappy_raw_lane(in, (int32_t)in_len, out, (int32_t)out_cap, (int32_t)hdr, (int32_t)(in_len + kInPad))
-               ? (int64_t)out_cap
-               : -1;
-#else
     BoundEmit em{out + out_cap};
     return snappy_raw(em, in, in_len, out, (uint32_t)out_cap, hdr) ? (int64_t)out_cap : -1;
-#endif
 }
 // The serial decoder's verdict for a planned body from its parts' decoded
 // sizes r(k) (-1: the part is corrupt): V_OK or V_ERROR with *len as the serial

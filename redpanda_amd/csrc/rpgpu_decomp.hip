@@ -139,31 +139,8 @@ size_t zws_offset(uint32_t n) { return counter_offset(n) + 256 + (size_t)decomp_
 size_t parts_offset(uint32_t n, uint32_t cap) {
     return (zws_offset(n) + ws_region(n, cap) + 255) & ~(size_t)255;
 }
-// the split zstd decoder's per-list-entry state (rpgpu_zseq.h), after the parts:
-// flag[n] u32 (bit 0 planned, 1 handed back, 2 execute) | lits[n] u64 | recs[n] u64
-// (local prefixes) | lit / rec block sums [nb] u64 each | section words [n][kMaxSec] u32
-size_t zseq_offset(uint32_t n, uint32_t cap) {
-    return (parts_offset(n, cap) + (size_t)part_cap(n) * (sizeof(SplitPart) + sizeof(int32_t)) + 255) & ~(size_t)255;
-}
-#ifdef RPZS_HBM_WS  // diagnostics build: A1 / A2 workspaces in HBM, one per zstd lane
-constexpr size_t kZsWs = sizeof(rpzstd::SeqWs) > sizeof(rpzstd::HufWs) ? sizeof(rpzstd::SeqWs) : sizeof(rpzstd::HufWs);
-#else
-constexpr size_t kZsWs = 0;
-#endif
-size_t zseq_bytes(uint32_t n) {
-    const size_t nb = (n + kScanBlock - 1) / kScanBlock;
-    return (size_t)n * (4 + 8 + 8 + 4 + 4 + 4 * rpzstd::kMaxSec) + 2 * nb * 8 + 64 +
-           (size_t)(n < RPZ_LANES ? n : RPZ_LANES) * ((kZsWs + 15) & ~(size_t)15);
-}
-struct ZParts {
-    uint8_t* hws;  // RPZS_HBM_WS: the lanes' workspaces
-    uint32_t* flag;
-    uint64_t *lits, *recs, *bs_l, *bs_r;  // exclusive prefixes within scan blocks, block prefixes
-    uint32_t *szl, *szr;                   // the plan's literal bytes / records per entry
-    uint32_t* sec;
-};
 // the block-parallel decoder of large zstd frames (rpgpu_zblk.h), after the
-// split decoder's state: per zstd wave list entry (the first kBlkFrames) its
+// parts: per zstd wave list entry (the first kBlkFrames) its
 // frame record, then a pool of kBlkPool blocks and each block's entry
 constexpr uint32_t kBlkFrames = 16384, kBlkPool = 65536;
 struct ZbFrame {
@@ -173,7 +150,9 @@ struct ZbFrame {
 };
 static_assert(sizeof(ZbFrame) == 48, "ZbFrame layout");
 uint32_t zb_frames(uint32_t n) { return n < kBlkFrames ? n : kBlkFrames; }
-size_t zblk_offset(uint32_t n, uint32_t cap) { return (zseq_offset(n, cap) + zseq_bytes(n) + 255) & ~(size_t)255; }
+size_t zblk_offset(uint32_t n, uint32_t cap) {
+    return (parts_offset(n, cap) + (size_t)part_cap(n) * (sizeof(SplitPart) + sizeof(int32_t)) + 255) & ~(size_t)255;
+}
 size_t zblk_bytes(uint32_t n) {
     return (size_t)zb_frames(n) * sizeof(ZbFrame) + (size_t)kBlkPool * (sizeof(rpzstd::Blk) + 4) + 256;
 }
@@ -188,21 +167,6 @@ ZbParts zbparts(void* p, uint32_t n, uint32_t cap) {
     z.pool = reinterpret_cast<rpzstd::Blk*>(b);
     z.frames = reinterpret_cast<ZbFrame*>(z.pool + kBlkPool);
     z.bframe = reinterpret_cast<uint32_t*>(z.frames + zb_frames(n));
-    return z;
-}
-ZParts zparts(void* p, uint32_t n, uint32_t cap) {
-    const size_t nb = (n + kScanBlock - 1) / kScanBlock;
-    uint8_t* b = static_cast<uint8_t*>(p) + zseq_offset(n, cap);
-    ZParts z;
-    z.lits = reinterpret_cast<uint64_t*>(b);
-    z.recs = z.lits + n;
-    z.bs_l = z.recs + n;
-    z.bs_r = z.bs_l + nb;
-    z.flag = reinterpret_cast<uint32_t*>(z.bs_r + nb);
-    z.szl = z.flag + n;
-    z.szr = z.szl + n;
-    z.sec = z.szr + n;
-    z.hws = reinterpret_cast<uint8_t*>((reinterpret_cast<uintptr_t>(z.sec + (size_t)n * rpzstd::kMaxSec) + 63) & ~(uintptr_t)63);
     return z;
 }
 Parts parts(void* p, uint32_t n, uint32_t cap) {
@@ -247,11 +211,13 @@ __device__ __forceinline__ uint64_t lane_max(uint32_t codec) { return codec == 4
 #define RPGPU_ZSTD_BLK_MIN (80u << 10)
 #endif
 constexpr uint64_t kZstdBlkMin = RPGPU_ZSTD_BLK_MIN;
-// the first frame's content size, 0 when it has none (or the body is no frame)
-__device__ __forceinline__ uint64_t zstd_content_size(const uint8_t* b, uint64_t n) {
+// the first frame's content size when the block-parallel decoder could take the
+// frame (no checksum, no dictionary: plan_blocks' header conditions), else 0 --
+// a lane-sized checksummed frame stays on the lanes, not the wave decoder
+__device__ __forceinline__ uint64_t zstd_blk_content(const uint8_t* b, uint64_t n) {
     if (n < 5 || rpcodec::le32(b) != rpzstd::kMagic) return 0;
     rpzstd::Frame h;
-    if (rpzstd::frame_header(b, n, h) != 0 || h.fcs == rpzstd::kUnknown) return 0;
+    if (rpzstd::frame_header(b, n, h) != 0 || h.fcs == rpzstd::kUnknown || h.csum || h.dict) return 0;
     return h.fcs;
 }
 // LZ4 / snappy-java slots above this are split into parts when the frame allows
@@ -270,9 +236,7 @@ static_assert(kSplitMinSlot <= kLaneMaxSlot, "split threshold above the lane dec
 // with out_len = the bound, the capacity a retry needs (rpgpu_decompress_batch)
 constexpr uint64_t kOverCeiling = 1ull << 63;
 
-// the split zstd decoder's per-entry flags (zseq_*_kernel below)
-constexpr uint32_t kZPlanned = 1, kZBack = 2, kZExec = 4, kZOver = 8;
-// zmode: bits 0..1 the split decoder (0 off, 1 LDS, 2 fused), bit 2 large frames on the wave decoder only
+// zmode: bit 2 large frames on the wave decoder only (RPGPU_OPT_ZSTD_WAVE_ONLY)
 constexpr uint32_t kZModeNoBlk = 4;
 __device__ __forceinline__ uint64_t cnt64(const uint32_t* c, int k) {
     return (uint64_t)c[k] | ((uint64_t)c[k + 1] << 32);
@@ -347,7 +311,7 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
         // them from C4's 66 KB frames) go to the wave list -- the block-parallel
         // decoder takes what it can plan, the wave decoder the rest
         if (wanted && !over && codec == 4)
-            zwave = sz > lane_max(4) || zstd_content_size(b, body) > kZstdBlkMin;
+            zwave = sz > lane_max(4) || zstd_blk_content(b, body) > kZstdBlkMin;
         if (wanted && !over && (codec == 2 || codec == 3) && sz > kSplitMinSlot) {
             auto none = [](uint32_t, uint32_t, uint64_t, uint64_t, uint64_t, uint64_t, uint32_t) {};
             np = codec == 3 ? rpcodec::lz4f_split(b, body, half, none) : rpcodec::snappy_java_split(b, body, half, none);
@@ -598,7 +562,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_WS_WA
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
     rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
     rpgpu_batch_desc* __restrict__ out_descs, void* __restrict__ wsraw, uint32_t* __restrict__ counter,
-    uint32_t* __restrict__ zlist, const uint32_t* __restrict__ zflag) {
+    uint32_t* __restrict__ zlist) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     // gzip: every batch index, 2 KB workspaces in the scratch; zstd: the plan's
     // list, `zl` workspaces after the output slots (decomp_ws_kernel)
@@ -617,8 +581,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_WS_WA
     if (g >= n || g >= lanes) return;  // lanes past the arena / the list own no workspace
     rpinfl::Ws& gws = reinterpret_cast<rpinfl::Ws*>(wsraw)[g];
     for (uint32_t k = g; k < cnt; k += lanes) {
-        // zstd: the split decoder's batches unless it handed them back
-        if (FAM == 4 && (zflag[k] & (kZPlanned | kZBack)) == kZPlanned) continue;
         const uint32_t i = FAM == 4 ? zlist[k] : k;
         const rpgpu_batch_desc d = descs[i];
         const rpgpu_batch_result v = vres[i];
@@ -685,242 +647,10 @@ __global__ __launch_bounds__(256) void zstd_ring_kernel(
 }
 
 
-// ---------------------------------------------------- split zstd decoder
-// (rpgpu_zseq.h).  Counters: [16..17] literal bytes planned, [18..19] records
-// planned (u64 totals of the scans), [20..21] / [22..23] the literal / record
-// regions' offsets in the output buffer (after the lane workspaces).
-// zflag per zstd lane list entry: bit 0 planned for the split path, 1 handed
-// back to the one-lane decoder, 2 execute (verdict OK), 3 A1 ran out of room.
-
-// per zstd lane list entry: eligibility and reservations, scanned per workgroup
-__global__ __launch_bounds__(kScanBlock) void zseq_plan_kernel(
-    const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data,
-    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot, const uint32_t* __restrict__ counter,
-    const uint32_t* __restrict__ zlist, uint32_t* __restrict__ flag, uint64_t* __restrict__ lits,
-    uint64_t* __restrict__ recs, uint64_t* __restrict__ bs_l, uint64_t* __restrict__ bs_r, uint32_t* __restrict__ szl,
-    uint32_t* __restrict__ szr, uint32_t n, bool enabled) {
-    __shared__ uint64_t wl[kScanBlock / 64], wr[kScanBlock / 64];
-    const uint32_t k = blockIdx.x * kScanBlock + threadIdx.x;
-    const uint32_t cnt = counter[7];
-    uint64_t a = 0, r = 0;
-    if (k < cnt) {
-        const uint32_t i = zlist[k];
-        const rpgpu_batch_desc d = descs[i];
-        const rpgpu_batch_result v = vres[i];
-        const uint64_t sz = slot[i];
-        uint32_t f = 0;
-        if (enabled && decomp_wanted(d, v) && v.codec == 4 && !(sz & kOverCeiling) && sz != 0 && sz <= lane_max(4)) {
-            const rpzstd::Plan pl = rpzstd::plan(data + d.offset + kHeaderSize, body_len(v));
-            if (pl.ok && pl.lits < (1ull << 31) && pl.recs < (1ull << 31)) {
-                f = kZPlanned;
-                a = pl.lits;
-                r = pl.recs;
-            }
-        }
-        flag[k] = f;
-        szl[k] = (uint32_t)a;
-        szr[k] = (uint32_t)r;
-    }
-    const uint32_t l = lane_id();
-    uint64_t x = a, y = r;
-#pragma unroll
-    for (int s = 1; s < 64; s <<= 1) {
-        const uint32_t lo = __shfl_up((uint32_t)x, s, 64), hi = __shfl_up((uint32_t)(x >> 32), s, 64);
-        const uint32_t plo = __shfl_up((uint32_t)y, s, 64), phi = __shfl_up((uint32_t)(y >> 32), s, 64);
-        if (l >= (uint32_t)s) {
-            x += ((uint64_t)hi << 32) | lo;
-            y += ((uint64_t)phi << 32) | plo;
-        }
-    }
-    const uint32_t wv = threadIdx.x >> 6;
-    if (l == 63) {
-        wl[wv] = x;
-        wr[wv] = y;
-    }
-    __syncthreads();
-    uint64_t bl = 0, br = 0;
-    for (uint32_t q = 0; q < wv; q++) {
-        bl += wl[q];
-        br += wr[q];
-    }
-    if (k < n) {
-        lits[k] = bl + x - a;
-        recs[k] = br + y - r;
-    }
-    if (threadIdx.x == kScanBlock - 1) {
-        bs_l[blockIdx.x] = bl + x;
-        bs_r[blockIdx.x] = br + y;
-    }
-}
-
-// A1: literal sections (Huffman tables in LDS, one HufWs per lane)
-#ifdef RPZS_HBM_WS
-#define RPZS_WG 256
-#else
-#define RPZS_WG 64
-#endif
-__global__ __launch_bounds__(RPZS_WG) void zseq_lit_kernel(
-    const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data,
-    const rpgpu_batch_result* __restrict__ vres, const uint32_t* __restrict__ counter,
-    const uint32_t* __restrict__ zlist, uint32_t* __restrict__ flag, const uint64_t* __restrict__ lits,
-    const uint64_t* __restrict__ bs_l, const uint32_t* __restrict__ szl, uint32_t* __restrict__ sec_all,
-    uint8_t* __restrict__ out, uint32_t per_wg, uint8_t* __restrict__ hws) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
-    const uint32_t l = threadIdx.x;
-    if (l >= per_wg) return;
-#ifdef RPZS_HBM_WS
-    rpzstd::HufWs& w = *reinterpret_cast<rpzstd::HufWs*>(hws + (size_t)(blockIdx.x * per_wg + l) * ((kZsWs + 15) & ~(size_t)15));
-#else
-    rpzstd::HufWs& w = reinterpret_cast<rpzstd::HufWs*>(dyn_lds)[l];
-#endif
-    const uint32_t cnt = counter[7], lanes = gridDim.x * per_wg;
-    const uint64_t loff = cnt64(counter, 20);
-    for (uint32_t k = blockIdx.x * per_wg + l; k < cnt; k += lanes) {
-        if (!(flag[k] & kZPlanned)) continue;
-        const uint32_t i = zlist[k];
-        const rpgpu_batch_desc d = descs[i];
-        const rpgpu_batch_result v = vres[i];
-        uint32_t* sec = sec_all + (size_t)k * rpzstd::kMaxSec;
-        for (uint32_t j = 0; j < rpzstd::kMaxSec; j++) sec[j] = 0;
-        rpzstd::LitEmit em{out + loff + bs_l[k / kScanBlock] + lits[k], szl[k], 0, sec, -1, false};
-        rpzstd::lit_walk(em, w, data + d.offset + kHeaderSize, body_len(v));
-        flag[k] = kZPlanned | (em.over ? kZOver : 0u);
-    }
-}
-
-// A2: the restatement's decisions, copies written as records (SeqWs in LDS).
-// Decides the batch's verdict and decoded length, or hands it back.
-__global__ __launch_bounds__(RPZS_WG) void zseq_seq_kernel(
-    const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data,
-    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
-    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
-    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
-    rpgpu_batch_desc* __restrict__ out_descs, const uint32_t* __restrict__ counter,
-    const uint32_t* __restrict__ zlist, uint32_t* __restrict__ flag, const uint64_t* __restrict__ lits,
-    const uint64_t* __restrict__ bs_l, const uint32_t* __restrict__ szl, const uint64_t* __restrict__ recs,
-    const uint64_t* __restrict__ bs_r, const uint32_t* __restrict__ szr, const uint32_t* __restrict__ sec_all,
-    uint32_t per_wg, uint8_t* __restrict__ hws) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
-    const uint32_t l = threadIdx.x;
-    if (l >= per_wg) return;
-#ifdef RPZS_HBM_WS
-    rpzstd::SeqWs& w = *reinterpret_cast<rpzstd::SeqWs*>(hws + (size_t)(blockIdx.x * per_wg + l) * ((kZsWs + 15) & ~(size_t)15));
-#else
-    rpzstd::SeqWs& w = reinterpret_cast<rpzstd::SeqWs*>(dyn_lds)[l];
-#endif
-    const uint32_t cnt = counter[7], lanes = gridDim.x * per_wg;
-    const uint64_t loff = cnt64(counter, 20), roff = cnt64(counter, 22);
-    // the regions must lie inside the caller's buffer, else the one-lane decoder decides
-    const bool fits = roff + (cnt64(counter, 18) + 16) * 8 <= out_cap;
-    for (uint32_t k = blockIdx.x * per_wg + l; k < cnt; k += lanes) {
-        const uint32_t f = flag[k];
-        if (!(f & kZPlanned)) continue;
-        if (!fits) {
-            flag[k] = kZPlanned | kZBack;
-            continue;
-        }
-        const uint32_t i = zlist[k];
-        const rpgpu_batch_desc d = descs[i];
-        const rpgpu_batch_result v = vres[i];
-        uint64_t sz = slot[i];
-        const uint64_t off = block_base[i / kScanBlock] + local[i];
-        int32_t verdict = RPGPU_V_SKIPPED;
-        uint64_t len = 0;
-        uint32_t nf = kZPlanned;
-        if (plan_slot(sz, off, out_cap, verdict, len)) {
-            rpzstd::SeqEmit em{sec_all + (size_t)k * rpzstd::kMaxSec, -1, out + loff + bs_l[k / kScanBlock] + lits[k],
-                               szl[k], 0, reinterpret_cast<uint64_t*>(out + roff) + bs_r[k / kScanBlock] + recs[k],
-                               0, szr[k], nullptr, 0, (f & kZOver) != 0};
-            verdict = rpzstd::uncompress<false>(em, data + d.offset + kHeaderSize, body_len(v), out + off + kHeaderSize,
-                                                sz - kHeaderSize - rpcodec::kSlack, &len, w);
-            em.put(rpzstd::rec_op(rpzstd::kOpEnd, 0));
-            if (em.fb || verdict == rpzstd::V_RING) {
-                flag[k] = kZPlanned | kZBack;
-                continue;
-            }
-            if (verdict == RPGPU_V_OK) nf |= kZExec;
-        }
-        finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
-        flag[k] = nf;
-    }
-}
-
-// A1 + A2 fused: one lane per planned batch with the one-lane decoder's
-// workspace in HBM (the lane workspaces after the output slots, as
-// ws_lane_kernel's), Huffman literals into the literal region, copies as
-// records.  Decides the verdict and length, or hands the batch back.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_WS_WAVES))) void zseq_fused_kernel(
-    const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data,
-    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
-    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
-    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
-    rpgpu_batch_desc* __restrict__ out_descs, const uint32_t* __restrict__ counter,
-    const uint32_t* __restrict__ zlist, uint32_t* __restrict__ flag, const uint64_t* __restrict__ lits,
-    const uint64_t* __restrict__ bs_l, const uint32_t* __restrict__ szl, const uint64_t* __restrict__ recs,
-    const uint64_t* __restrict__ bs_r, const uint32_t* __restrict__ szr) {
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t cnt = counter[7];
-    const uint32_t lanes = counter[10] < gridDim.x * blockDim.x ? counter[10] : gridDim.x * blockDim.x;
-    if (g >= lanes) return;
-    const uint64_t ws_off = cnt64(counter, 8), loff = cnt64(counter, 20), roff = cnt64(counter, 22);
-    rpzstd::Ws& w = reinterpret_cast<rpzstd::Ws*>(out + ws_off)[g];
-    const bool fits = roff + (cnt64(counter, 18) + 16) * 8 <= out_cap;
-    for (uint32_t k = g; k < cnt; k += lanes) {
-        const uint32_t f = flag[k];
-        if (!(f & kZPlanned)) continue;
-        if (!fits) {
-            flag[k] = kZPlanned | kZBack;
-            continue;
-        }
-        const uint32_t i = zlist[k];
-        const rpgpu_batch_desc d = descs[i];
-        const rpgpu_batch_result v = vres[i];
-        uint64_t sz = slot[i];
-        const uint64_t off = block_base[i / kScanBlock] + local[i];
-        int32_t verdict = RPGPU_V_SKIPPED;
-        uint64_t len = 0;
-        uint32_t nf = kZPlanned;
-        if (plan_slot(sz, off, out_cap, verdict, len)) {
-            rpzstd::RecEmit em{{nullptr, -1, out + loff + bs_l[k / kScanBlock] + lits[k], szl[k], 0,
-                                reinterpret_cast<uint64_t*>(out + roff) + bs_r[k / kScanBlock] + recs[k], 0, szr[k],
-                                nullptr, 0, false}};
-            verdict = rpzstd::uncompress<false>(em, data + d.offset + kHeaderSize, body_len(v), out + off + kHeaderSize,
-                                                sz - kHeaderSize - rpcodec::kSlack, &len, w);
-            em.put(rpzstd::rec_op(rpzstd::kOpEnd, 0));
-            if (em.fb || verdict == rpzstd::V_RING) {
-                flag[k] = kZPlanned | kZBack;
-                continue;
-            }
-            if (verdict == RPGPU_V_OK) nf |= kZExec;
-        }
-        finish_batch(i, d, v, off, sz, verdict, len, data, out, dres, out_descs);
-        flag[k] = nf;
-    }
-}
-
-// B: the records of every batch A2 decided OK, one lane per batch
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_WAVES))) void zseq_exec_kernel(
-    const uint32_t* __restrict__ counter, const uint32_t* __restrict__ zlist, const uint32_t* __restrict__ flag,
-    const uint64_t* __restrict__ recs, const uint64_t* __restrict__ bs_r, const uint64_t* __restrict__ local,
-    const uint64_t* __restrict__ block_base, uint8_t* __restrict__ out) {
-    const uint32_t cnt = counter[7], lanes = gridDim.x * blockDim.x;
-    const uint64_t roff = cnt64(counter, 22);
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += lanes) {
-        if ((flag[k] & (kZExec | kZBack)) != kZExec) continue;
-#ifdef RPZS_DIAG_NORECS
-        continue;
-#endif
-        const uint32_t i = zlist[k];
-        const uint64_t off = block_base[i / kScanBlock] + local[i];
-        RPZS_EXEC_CALL(reinterpret_cast<const uint64_t*>(out + roff) + bs_r[k / kScanBlock] + recs[k],
-                       out + off + kHeaderSize);
-    }
-}
-
 // ------------------------------------------- block-parallel zstd (large frames)
 // (rpgpu_zblk.h).  Counters: [24..25] literal bytes, [26..27] records planned
 // (u64), [28] pool blocks reserved, [30..31] / [32..33] the literal / record
-// regions' offsets in the output buffer (after the split decoder's).
+// regions' offsets in the output buffer (after the lane workspaces).
 __device__ __forceinline__ bool zb_fits(const uint32_t* counter, uint64_t out_cap) {
     return cnt64(counter, 32) + (cnt64(counter, 26) + 16) * 8 <= out_cap;
 }
@@ -1104,26 +834,17 @@ __global__ void decomp_ws_kernel(uint32_t* __restrict__ counter, uint32_t cap, u
     counter[8] = (uint32_t)off;
     counter[9] = (uint32_t)(off >> 32);
     counter[10] = lanes;
-    // the split decoder's literal and record regions (64 bytes / 16 records of padding)
     const uint64_t ws_end = lanes ? off + (uint64_t)lanes * sizeof(rpzstd::Ws) : slots;
-    const uint64_t loff = (ws_end + 255) & ~(uint64_t)255;
-    const uint64_t roff = (loff + cnt64(counter, 16) + 64 + 255) & ~(uint64_t)255;
-    counter[20] = (uint32_t)loff;
-    counter[21] = (uint32_t)(loff >> 32);
-    counter[22] = (uint32_t)roff;
-    counter[23] = (uint32_t)(roff >> 32);
-    // no batch planned for the split decoder (it is off, or no body qualified): no regions
-    const bool split = cnt64(counter, 18) != 0;
-    const uint64_t send = split ? roff + (cnt64(counter, 18) + 16) * 8 : ws_end;
-    // the block-parallel decoder's literal and record regions, likewise
-    const uint64_t bl = (send + 255) & ~(uint64_t)255;
+    // the block-parallel decoder's literal and record regions (64 bytes / 16
+    // records of padding)
+    const uint64_t bl = (ws_end + 255) & ~(uint64_t)255;
     const uint64_t br = (bl + cnt64(counter, 24) + 64 + 255) & ~(uint64_t)255;
     counter[30] = (uint32_t)bl;
     counter[31] = (uint32_t)(bl >> 32);
     counter[32] = (uint32_t)br;
     counter[33] = (uint32_t)(br >> 32);
     const bool blk = counter[28] != 0;
-    if (out_bytes) *out_bytes = blk ? br + (cnt64(counter, 26) + 16) * 8 : send;
+    if (out_bytes) *out_bytes = blk ? br + (cnt64(counter, 26) + 16) * 8 : ws_end;
 }
 
 // One batch body through the codec restatement, bytes produced by the wave.
@@ -1311,44 +1032,15 @@ __global__ void decomp_counters_kernel(uint32_t* c, uint32_t run) {
 }
 
 // ------------------------------------------------------------ launchers
-// the split zstd decoder's LDS geometry: RPZS_WAVES one-wave workgroups per CU
-// share the CU's LDS, each with as many lanes as their workspaces fit in its
-// share (RPZS_LDS_BYTES overrides the CU's LDS size).  The lanes decode serial
-// chains at LDS latency: spread over waves (two per SIMD) they hide each
-// other's latency, where one wave of 56 lanes per CU would not.
-struct ZLaunch {
-    uint32_t grid, lit_lanes, seq_lanes;
-};
-#ifndef RPZS_LDS_BYTES
-#define RPZS_LDS_BYTES 0
+// the block-parallel decoder's entropy lanes: RPGPU_ZBLK_WAVES one-wave
+// workgroups per CU share the CU's LDS, each with as many lanes as their
+// workspaces fit in its share.  The lanes decode serial chains at LDS latency:
+// spread over waves (two per SIMD) they hide each other's latency, where one
+// wave of 56 lanes per CU would not.
+#ifndef RPGPU_ZBLK_WAVES
+#define RPGPU_ZBLK_WAVES 8
 #endif
-#ifndef RPZS_WAVES
-#define RPZS_WAVES 8
-#endif
-ZLaunch zseq_launch() {
-    static ZLaunch z{0, 0, 0};
-    if (z.grid) return z;
-    int dev = 0, cus = 0, lds = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
-    if (RPZS_LDS_BYTES) lds = RPZS_LDS_BYTES;
-    if (lds < (int)sizeof(rpzstd::SeqWs)) lds = (int)sizeof(rpzstd::SeqWs);
-    auto fit = [&](size_t each) {
-        const size_t k = (size_t)lds / RPZS_WAVES / each;
-        return (uint32_t)(k > 64 ? 64 : k < 1 ? 1 : k);
-    };
-    ZLaunch t{(uint32_t)((cus > 0 ? cus : 256) * RPZS_WAVES), fit(sizeof(rpzstd::HufWs)), fit(sizeof(rpzstd::SeqWs))};
-    hipFuncSetAttribute(reinterpret_cast<const void*>(zseq_lit_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)(t.lit_lanes * sizeof(rpzstd::HufWs)));
-    hipFuncSetAttribute(reinterpret_cast<const void*>(zseq_seq_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)(t.seq_lanes * sizeof(rpzstd::SeqWs)));
-    z = t;
-    return z;
-}
-
-// the block-parallel decoder's entropy lanes: as the split decoder's, one
-// ZbWs (Huffman or FSE tables) per lane in LDS
+// one ZbWs (Huffman or FSE tables) per lane
 struct ZbLaunch {
     uint32_t grid, lanes;
 };
@@ -1360,9 +1052,9 @@ ZbLaunch zblk_launch() {
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
     if (lds < (int)sizeof(ZbWs)) lds = (int)sizeof(ZbWs);
-    size_t k = (size_t)lds / RPZS_WAVES / sizeof(ZbWs);
+    size_t k = (size_t)lds / RPGPU_ZBLK_WAVES / sizeof(ZbWs);
     k = k > 64 ? 64 : (k < 1 ? 1 : k);
-    ZbLaunch t{(uint32_t)((cus > 0 ? cus : 256) * RPZS_WAVES), (uint32_t)k};
+    ZbLaunch t{(uint32_t)((cus > 0 ? cus : 256) * RPGPU_ZBLK_WAVES), (uint32_t)k};
     hipFuncSetAttribute(reinterpret_cast<const void*>(zblk_entropy_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)(t.lanes * sizeof(ZbWs)));
     z = t;
@@ -1400,13 +1092,6 @@ hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const
                                                                    !(zmode & kZModeNoBlk));
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    // the split zstd decoder's reservations over the zstd lane list
-    const ZParts z = zparts(d_scratch, n, ws_cap);
-    zseq_plan_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, d_data, d_vres, p.slot, p.counter, p.wlist + 2 * (size_t)n,
-                                               z.flag, z.lits, z.recs, z.bs_l, z.bs_r, z.szl, z.szr, n, (zmode & 3) != 0);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = launch_block_scan(z.bs_l, nb, reinterpret_cast<uint64_t*>(p.counter + 16), s)) != hipSuccess) return e;
-    if ((e = launch_block_scan(z.bs_r, nb, reinterpret_cast<uint64_t*>(p.counter + 18), s)) != hipSuccess) return e;
     if ((e = launch_block_scan(p.block_sum, nb, reinterpret_cast<uint64_t*>(p.counter + 8), s)) != hipSuccess) return e;
     decomp_ws_kernel<<<1, 64, 0, s>>>(p.counter, zstd_lanes(n, ws_cap), d_out_bytes);
     return hipGetLastError();
@@ -1452,41 +1137,9 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     auto zlanes_zstd = [&]() -> hipError_t {
         hipError_t e = hipSuccess;
         const uint32_t zl = zstd_lanes(n, ws_cap);  // the HBM-workspace lane decoder (at most zl lanes)
-        // the split decoder over the zstd lane batches it planned: A1 literals, A2
-        // decisions + records, B execution; what A2 hands back, the one-lane decoder
-        const ZParts z = zparts(d_scratch, n, ws_cap);
-        if ((zmode & 3) == 2) {
-            zseq_fused_kernel<<<(zl + 255) / 256, 256, 0, zs>>>(
-                d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.counter,
-                p.wlist + 2 * (size_t)n, z.flag, z.lits, z.bs_l, z.szl, z.recs, z.bs_r, z.szr);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-            zseq_exec_kernel<<<(zl + 255) / 256, 256, 0, zs>>>(p.counter, p.wlist + 2 * (size_t)n, z.flag, z.recs, z.bs_r,
-                                                             p.local, p.block_sum, d_out);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-        } else if ((zmode & 3) == 1) {
-    #ifdef RPZS_HBM_WS
-            const uint32_t zl_n = n < RPZ_LANES ? n : RPZ_LANES;
-            const ZLaunch zq{(zl_n + 255) / 256, 256, 256};
-            const size_t lit_lds = 0, seq_lds = 0;
-    #else
-            const ZLaunch zq = zseq_launch();
-            const size_t lit_lds = zq.lit_lanes * sizeof(rpzstd::HufWs), seq_lds = zq.seq_lanes * sizeof(rpzstd::SeqWs);
-    #endif
-            zseq_lit_kernel<<<zq.grid, RPZS_WG, lit_lds, zs>>>(
-                d_descs, d_data, d_vres, p.counter, p.wlist + 2 * (size_t)n, z.flag, z.lits, z.bs_l, z.szl, z.sec, d_out,
-                zq.lit_lanes, z.hws);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-            zseq_seq_kernel<<<zq.grid, RPZS_WG, seq_lds, zs>>>(
-                d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.counter,
-                p.wlist + 2 * (size_t)n, z.flag, z.lits, z.bs_l, z.szl, z.recs, z.bs_r, z.szr, z.sec, zq.seq_lanes, z.hws);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-            zseq_exec_kernel<<<(zl + 255) / 256, 256, 0, zs>>>(p.counter, p.wlist + 2 * (size_t)n, z.flag, z.recs, z.bs_r,
-                                                             p.local, p.block_sum, d_out);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-        }
         ws_lane_kernel<4><<<(zl + 255) / 256, 256, 0, zs>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres,
                                                              d_out, out_cap, d_out_descs, nullptr, p.counter,
-                                                             p.wlist + 2 * (size_t)n, z.flag);
+                                                             p.wlist + 2 * (size_t)n);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         zstd_ring_kernel<<<(zl + 255) / 256, 256, 0, zs>>>(d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres,
                                                           d_out, out_cap, d_out_descs, p.counter, p.wlist + 2 * (size_t)n);
@@ -1500,7 +1153,7 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
             const uint32_t gl = gzip_lanes(n, ws_cap);
             ws_lane_kernel<1><<<(gl + 255) / 256, 256, 0, zs>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
                                                                  p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.gws,
-                                                                 p.counter, nullptr, nullptr);
+                                                                 p.counter, nullptr);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
         return hipSuccess;

@@ -32,18 +32,15 @@ class Engine:
 
     def __init__(self, device: int = 0, max_decoded_batch: int = 0, walk_overlap: bool = True,
                  decomp_ws_lanes: int = 0, walk_chunks: int = 0, blocks_per_cu: int = 0,
-                 zstd_split: bool | str = False, zstd_blocks: bool = True):
+                 zstd_blocks: bool = True):
         """walk_overlap: the record walk beside the checksums (the default; False sets
         RPGPU_OPT_NO_WALK_OVERLAP);
         decomp_ws_lanes: rpgpu_opts.decomp_ws_lanes (0: the default ceiling);
         walk_chunks / blocks_per_cu: rpgpu_opts tuning fields (0: defaults);
-        zstd_split: True / "lds": the split zstd decoder (RPGPU_OPT_ZSTD_SPLIT); "fused":
-        RPGPU_OPT_ZSTD_FUSED; False: the one-lane decoder;
         zstd_blocks: large zstd frames block-parallel (the default; False sets
         RPGPU_OPT_ZSTD_WAVE_ONLY)."""
         self._lib = abi.lib()
         flags = (abi.OPT_WALK_OVERLAP if walk_overlap else abi.OPT_NO_WALK_OVERLAP) | \
-            (abi.OPT_ZSTD_FUSED if zstd_split == "fused" else abi.OPT_ZSTD_SPLIT if zstd_split else 0) | \
             (0 if zstd_blocks else abi.OPT_ZSTD_WAVE_ONLY)
         opts = abi.Opts(flags, 0, 0, max_decoded_batch, decomp_ws_lanes,
                         walk_chunks, blocks_per_cu)
@@ -680,6 +677,19 @@ class Engine:
 
 
 # ---- workload construction (librpgen.so) -----------------------------------------
+def library_hash() -> str | None:
+    """First 16 hex digits of the SHA-256 of the engine library this process
+    loads (RPGPU_DIAG_LIB or redpanda_amd/librpgpu.so): the key under which
+    profiles/traffic.json records PMC passes."""
+    import hashlib
+
+    path = os.environ.get("RPGPU_DIAG_LIB", str(abi.PKG / "librpgpu.so"))
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def make_spec(**kw) -> abi.GenSpec:
     s = abi.GenSpec()
     defaults = dict(seed=0x5EED0002, partitions=1, records_per_batch=16, key_len=16, value_len=995,

@@ -42,8 +42,7 @@ namespace {
 typedef std::vector<uint8_t> Bytes;
 std::mt19937_64 rng;
 uint64_t below(uint64_t n) { return n ? rng() % n : 0; }
-long n_cases = 0, n_ok = 0, n_rejected = 0, n_ring = 0, n_split = 0, n_split_fb = 0, n_split_no = 0,
-     n_blk = 0, n_blk_ok = 0;
+long n_cases = 0, n_ok = 0, n_rejected = 0, n_ring = 0, n_blk = 0, n_blk_ok = 0;
 
 void fail(const char* what) {
     fprintf(stderr, "FAIL: %s\n", what);
@@ -288,77 +287,6 @@ void mutate(Bytes& f) {
 
 bool g_exact = false;
 
-// The split decoder (rpgpu_zseq.h: A1 literals, A2 sequences to records, B
-// execution) against the one-lane decoder's first pass: same verdict, length
-// and bytes whenever A2 does not hand the batch back.
-void compare_split(const uint8_t* ip, size_t n, uint64_t cap, int32_t ev, uint64_t elen, const Bytes& eout) {
-    const rpzstd::Plan pl = rpzstd::plan(ip, n);
-    if (!pl.ok) {
-        n_split_no++;
-        return;
-    }
-    static rpzstd::HufWs hw;
-    static rpzstd::SeqWs sw;
-    Bytes lits(pl.lits + 64);
-    for (auto& c : lits) c = (uint8_t)rng();
-    uint32_t sec[rpzstd::kMaxSec];
-    for (auto& w : sec) w = 0;
-    rpzstd::LitEmit le{lits.data(), pl.lits, 0, sec, -1, false};
-    rpzstd::lit_walk(le, hw, ip, n);
-    std::vector<uint64_t> rec(pl.recs + 8);
-    rpzstd::SeqEmit se{sec, -1, lits.data(), pl.lits, 0, rec.data(), 0, pl.recs, nullptr, 0, le.over};
-    Bytes sout(cap + rpcodec::kSlack);
-    for (auto& c : sout) c = (uint8_t)rng();
-    uint64_t slen = 0;
-    const int32_t sv = rpzstd::uncompress<false>(se, ip, n, sout.data(), cap, &slen, sw);
-    se.put(rpzstd::rec_op(rpzstd::kOpEnd, 0));
-    if (se.fb || sv == rpzstd::V_RING) {
-        n_split_fb++;
-        return;
-    }
-    n_split++;
-    // the fused form (RecEmit over the one-lane workspace) must make the same records' worth of bytes
-    {
-        static rpzstd::Ws fw;
-        std::vector<uint64_t> frec(pl.recs + 8);
-        Bytes flits(pl.lits + 64), fout(cap + rpcodec::kSlack);
-        rpzstd::RecEmit fe{{nullptr, -1, flits.data(), pl.lits, 0, frec.data(), 0, pl.recs, nullptr, 0, false}};
-        uint64_t flen = 0;
-        const int32_t fv = rpzstd::uncompress<false>(fe, ip, n, fout.data(), cap, &flen, fw);
-        fe.put(rpzstd::rec_op(rpzstd::kOpEnd, 0));
-        bool fsame = !fe.fb && fv == ev && (fv != 0 || flen == elen);
-        if (fsame && fv == 0) {
-            rpzstd::exec_lane(frec.data(), fout.data());
-            fsame = !memcmp(fout.data(), eout.data(), flen);
-        }
-        if (!fsame) {
-            fprintf(stderr, "case %ld: fused v=%d len=%llu fb=%d, one-lane v=%d len=%llu\n", n_cases, fv,
-                    (unsigned long long)flen, (int)fe.fb, ev, (unsigned long long)elen);
-            exit(1);
-        }
-    }
-    bool same = sv == ev && (sv != 0 || slen == elen);
-    if (same && sv == 0) {
-        rpzstd::exec_lane(rec.data(), sout.data());
-        same = !memcmp(sout.data(), eout.data(), slen);
-    }
-    if (!same) {
-        fprintf(stderr, "case %ld: split v=%d len=%llu, one-lane v=%d len=%llu, input %zu bytes, %llu records\n",
-                n_cases, sv, (unsigned long long)slen, ev, (unsigned long long)elen, n,
-                (unsigned long long)se.nrec);
-        if (sv == 0 && ev == 0) {
-            size_t k = 0;
-            while (k < slen && sout[k] == eout[k]) k++;
-            fprintf(stderr, "first differing byte %zu\n", k);
-        }
-        FILE* fp = fopen("zstd_fuzz_fail.bin", "wb");
-        if (fp) {
-            fwrite(ip, 1, n, fp);
-            fclose(fp);
-        }
-        exit(1);
-    }
-}
 
 // The block-parallel path for large frames (rpgpu_zblk.h: plan, per-block
 // literals and sequences, serial resolve, execution) against the decoder's
@@ -448,7 +376,6 @@ void compare(const Bytes& in) {
     // as the device does: the lane pass (no ring history), then the ring pass
     // for a body whose ring wrapped (rpgpu_decomp.hip zstd_ring_kernel)
     int32_t ev = rpzstd::uncompress<false>(em, ip, in.size(), eout.data(), cap, &elen, ws);
-    if (ev != rpzstd::V_RING) compare_split(ip, in.size(), cap, ev, elen, eout);
     if (ev == rpzstd::V_RING) {
         n_ring++;
         ev = rpzstd::uncompress<true>(em, ip, in.size(), eout.data(), cap, &elen, ws);
@@ -820,7 +747,7 @@ int main(int argc, char** argv) {
         while ((c = fgetc(fp)) != EOF) in.push_back((uint8_t)c);
         fclose(fp);
         compare(in);
-        printf("replay: engine == oracle (split decoder: %ld compared, %ld handed back, %ld not planned)\n", n_split, n_split_fb, n_split_no);
+        printf("replay: engine == oracle\n");
         return 0;
     }
     check_select();
@@ -841,8 +768,6 @@ int main(int argc, char** argv) {
     }
     printf("zstd fuzz: %ld cases (%ld through the ring pass), %ld decoded, %ld rejected: engine == oracle\n",
            n_cases, n_ring, n_ok, n_rejected);
-    printf("split decoder: %ld cases == one-lane decoder, %ld handed back, %ld not planned\n", n_split, n_split_fb,
-           n_split_no);
     printf("block-parallel path: %ld large frames planned, %ld decoded: == decoder\n", n_blk, n_blk_ok);
     return 0;
 }
