@@ -135,6 +135,29 @@ constexpr uint16_t kAlgoTime[16][2][2] = {
     {{926, 128}, {1613, 75}},  {{947, 128}, {1729, 77}},  {{1107, 128}, {2083, 81}}, {{1177, 128}, {2379, 87}},
     {{1242, 128}, {2415, 93}}, {{1349, 128}, {2644, 106}}, {{1455, 128}, {2422, 124}}, {{722, 128}, {1891, 145}}};
 
+// kLLBase[c] | kLLBits[c] << 24 and kMLBase[c] | kMLBits[c] << 24 from the
+// code alone: the lane decoder's sequence loop then issues no dependent load
+// (a constant-table lookup behind each FSE cell's) per sequence.  Codes below
+// 16 / 32 have no extra bits, codes from 25 / 43 on are powers of two (+3);
+// the few between come from packed constants.  Pinned against the tables by
+// tests/native/zstd_fuzz.cpp check_xcalc.
+RPC_HD uint32_t ll_x(uint32_t c) {  // c <= 35
+    if (c < 16) return c;
+    if (c >= 25) return (1u << (c - 19)) | ((c - 19) << 24);
+    const uint32_t j = c - 16;
+    const uint32_t bits = (uint32_t)(0x433221111ull >> (4 * j)) & 15u;
+    const uint32_t base = j < 8 ? (uint32_t)(0x28201C1816141210ull >> (8 * j)) & 255u : 48u;
+    return base | (bits << 24);
+}
+RPC_HD uint32_t ml_x(uint32_t c) {  // c <= 52
+    if (c < 32) return c + 3;
+    if (c >= 43) return ((1u << (c - 36)) + 3) | ((c - 36) << 24);
+    const uint32_t j = c - 32;
+    const uint32_t bits = (uint32_t)(0x54433221111ull >> (4 * j)) & 15u;
+    const uint32_t d = j < 8 ? (uint32_t)(0x18100C0806040200ull >> (8 * j)) & 255u
+                             : (uint32_t)(0x403020ull >> (8 * (j - 8))) & 255u;
+    return (35 + d) | (bits << 24);
+}
 RPC_HD uint32_t hb32(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }  // BIT_highbit32, v > 0
 RPC_HD uint32_t le24(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16); }
 RPC_HD uint64_t lomask(uint32_t n) { return n >= 64 ? ~0ull : ((1ull << n) - 1); }
@@ -254,6 +277,9 @@ RPC_HD void copy_seq_match(uint8_t* dst, uint64_t off, uint64_t n) {
 // the output, `lp`), where the exact copies above run instead.
 #ifndef RPGPU_ZSTD_WC
 #define RPGPU_ZSTD_WC 1
+#endif
+#ifndef RPGPU_ZSTD_XCALC  // sequence code baselines computed (ll_x / ml_x), not looked up
+#define RPGPU_ZSTD_XCALC 1
 #endif
 struct WcBuf {
     rpcodec::V16 cur, cur1;
@@ -1408,8 +1434,13 @@ RPZ_COLD int64_t block(E& em, W& w, const uint8_t* in, uint64_t n, uint8_t* out,
                 xLL = w.llx[sLL];
                 xML = w.mlx[sML];
             } else {
+#if RPGPU_ZSTD_XCALC
+                xLL = ll_x(cLL);
+                xML = ml_x(cML);
+#else
                 xLL = kLLBase[cLL] | ((uint32_t)kLLBits[cLL] << 24);
                 xML = kMLBase[cML] | ((uint32_t)kMLBits[cML] << 24);
+#endif
             }
             const uint32_t cOF = eOF & 0xFF;
             const uint32_t llBase = xLL & 0xFFFFFF, mlBase = xML & 0xFFFFFF;

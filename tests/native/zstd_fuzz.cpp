@@ -287,6 +287,20 @@ void mutate(Bytes& f) {
 
 bool g_exact = false;
 
+// the computed sequence baselines (rpzstd::ll_x / ml_x) against the tables
+void check_xcalc() {
+    for (uint32_t c = 0; c < 36; c++)
+        if (rpzstd::ll_x(c) != (rpzstd::kLLBase[c] | ((uint32_t)rpzstd::kLLBits[c] << 24))) {
+            fprintf(stderr, "ll_x(%u) = %#x\n", c, rpzstd::ll_x(c));
+            exit(1);
+        }
+    for (uint32_t c = 0; c < 53; c++)
+        if (rpzstd::ml_x(c) != (rpzstd::kMLBase[c] | ((uint32_t)rpzstd::kMLBits[c] << 24))) {
+            fprintf(stderr, "ml_x(%u) = %#x\n", c, rpzstd::ml_x(c));
+            exit(1);
+        }
+}
+
 
 // The block-parallel path for large frames (rpgpu_zblk.h: plan, per-block
 // literals and sequences, serial resolve, execution) against the decoder's
@@ -655,6 +669,74 @@ Bytes band_frame(int nblocks = 0) {
     return f;
 }
 
+// A match spanning the previous ring segment's end into the current one close
+// to the current segment's start: frames with a 1 KiB window
+// (segments [0, 2048), [2048, 4096), ...) whose block 2 -- the first of the
+// second segment -- opens with `lead` sequences of short literal runs and
+// matches inside the segment, then one of `ll` literals and a match of
+// len1 + m2 bytes whose first len1 bytes are the extDict's last ones: at
+// distance lw + len1 from the segment's start (lw = bytes of the segment
+// before the match), i.e. a second part copied from the segment's start at a
+// distance lw + len1 that may be below 16 (libzstd's overlapCopy8) or not.
+Bytes span_frame(uint32_t lead, uint32_t ll, uint32_t len1, uint32_t m2) {
+    Bytes f = {0x28, 0xB5, 0x2F, 0xFD, 0x00, 0x00};  // no FCS / checksum; window 1 KiB
+    for (int k = 0; k < 4; k++) {
+        Bytes lits;
+        std::vector<rpzstdc::Seq> seqs;
+        uint32_t produced = 0;
+        if (k == 2) {
+            uint32_t pos = 0;  // within the segment
+            for (uint32_t q = 0; q < lead; q++) {
+                const uint32_t l = (uint32_t)below(6), m = 3 + (uint32_t)below(6);
+                for (uint32_t j = 0; j < l; j++) lits.push_back((uint8_t)('a' + below(26)));
+                const uint32_t off = pos + l == 0 ? 0 : 1 + (uint32_t)below(pos + l);
+                if (off == 0) {  // nothing to reach back to inside the segment yet: literals only
+                    lits.push_back('z');
+                    seqs.push_back(rpzstdc::Seq{l + 1, m, l + 1});
+                    pos += l + 1 + m;
+                    produced += l + 1 + m;
+                    continue;
+                }
+                seqs.push_back(rpzstdc::Seq{l, m, off});
+                pos += l + m;
+                produced += l + m;
+            }
+            for (uint32_t j = 0; j < ll; j++) lits.push_back((uint8_t)('a' + below(26)));
+            const uint32_t lw = pos + ll;
+            const uint32_t ml = len1 + m2 < 3 ? 3 : len1 + m2;  // MINMATCH
+            seqs.push_back(rpzstdc::Seq{ll, ml, lw + len1});
+            produced += ll + ml;
+        } else {
+            for (int j = 0; j < 1000; j++) lits.push_back((uint8_t)('A' + (rng() % 16)));
+            seqs.push_back(rpzstdc::Seq{900, 24, 1 + (uint32_t)below(k == 0 ? 899 : 1000)});
+            produced = 924;
+        }
+        const uint32_t target = 1024;
+        for (uint32_t j = produced; j < target; j++) lits.push_back((uint8_t)('a' + below(26)));
+        const Bytes blk = seq_block(lits, seqs);
+        const uint32_t last = k + 1 == 4 ? 1u : 0u;
+        const uint32_t bh = last | (2u << 1) | ((uint32_t)blk.size() << 3);
+        f.push_back((uint8_t)bh), f.push_back((uint8_t)(bh >> 8)), f.push_back((uint8_t)(bh >> 16));
+        f.insert(f.end(), blk.begin(), blk.end());
+    }
+    return f;
+}
+
+long n_span = 0;
+void check_span(long cases) {
+    for (uint32_t lead : {0u, 1u, 3u})
+        for (uint32_t ll : {0u, 1u, 5u, 15u, 16u, 17u})
+            for (uint32_t len1 : {1u, 2u, 7u, 8u, 9u, 15u, 16u, 17u, 40u})
+                for (uint32_t m2 : {1u, 3u, 8u, 15u, 16u, 17u, 33u, 80u}) {
+                    compare(span_frame(lead, ll, len1, m2));
+                    n_span++;
+                }
+    for (long i = 0; i < cases; i++) {
+        compare(span_frame((uint32_t)below(5), (uint32_t)below(40), 1 + (uint32_t)below(100), 1 + (uint32_t)below(100)));
+        n_span++;
+    }
+}
+
 void check_band(long cases) {
     const long ok0 = n_ok, rej0 = n_rejected;
     for (long i = 0; i < cases; i++) {
@@ -750,9 +832,11 @@ int main(int argc, char** argv) {
         printf("replay: engine == oracle\n");
         return 0;
     }
+    check_xcalc();
     check_select();
     check_windows();
     check_ring_crafted();
+    check_span(cases / 4 + 1);
     check_band(cases / 2 + 1);
     check_ring(cases / 8 + 1);
     check_ncount(cases * 4);
@@ -769,5 +853,6 @@ int main(int argc, char** argv) {
     printf("zstd fuzz: %ld cases (%ld through the ring pass), %ld decoded, %ld rejected: engine == oracle\n",
            n_cases, n_ring, n_ok, n_rejected);
     printf("block-parallel path: %ld large frames planned, %ld decoded: == decoder\n", n_blk, n_blk_ok);
+    printf("span frames (a match across the ring segments' boundary near the segment start): %ld == libzstd\n", n_span);
     return 0;
 }
