@@ -252,6 +252,9 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
                        hipEventCreateWithFlags(&c->dstreams.join2, hipEventDisableTiming) == hipSuccess &&
                        hipEventCreateWithFlags(&c->dstreams.lanes, hipEventDisableTiming) == hipSuccess &&
                        hipEventCreateWithFlags(&c->dstreams.parts, hipEventDisableTiming) == hipSuccess;
+    // diagnostics: every decompression kernel on the one stream, one after the
+    // other (each kernel's duration alone, in a kernel trace)
+    if (const char* ss = getenv("RPGPU_SERIAL_STREAMS"); ss && ss[0] == '1') c->have_dstreams = false;
     c->have_overlap = hipStreamCreateWithFlags(&c->overlap.aux, hipStreamNonBlocking) == hipSuccess;
     for (int k = 0; c->have_overlap && k <= c->overlap.chunks; k++)
         c->have_overlap = hipEventCreateWithFlags(&c->overlap.ev[k], hipEventDisableTiming) == hipSuccess;
@@ -563,6 +566,20 @@ int32_t rpgpu_decomp_run_device(rpgpu_ctx* c, const rpgpu_batch_desc* d_descs, u
                                             c->have_overlap ? &c->overlap : nullptr,
                                             c->have_dstreams ? &c->dstreams : nullptr, pc);
     if (e != hipSuccess) return fail(c, e, "decomp run launch");
+    // diagnostics: the plan's counts and, after the run, the LZ wave list's final
+    // length (split fallbacks included) on stderr
+    static const bool trace = getenv("RPGPU_PLAN_TRACE") != nullptr;
+    if (trace && n) {
+        uint32_t after[64];
+        const uint8_t* cnt = static_cast<const uint8_t*>(d_scratch) + rpgpu::decomp_counter_offset(n, c->ws_lanes);
+        if (hipMemcpyAsync(after, cnt, sizeof(after), hipMemcpyDeviceToHost, s) == hipSuccess &&
+            hipStreamSynchronize(s) == hipSuccess)
+            fprintf(stderr,
+                    "rpgpu plan n=%u: zwave %u lz4parts %u snappyparts %u lzwave %u zlane %u snappylane %u "
+                    "gzip %u zblk %u/%u | after: lzwave %u\n",
+                    n, pc ? pc[2] : 0u, pc ? pc[4] : 0u, pc ? pc[5] : 0u, pc ? pc[6] : 0u, pc ? pc[7] : 0u,
+                    pc ? pc[12] : 0u, pc ? pc[13] : 0u, pc ? pc[28] : 0u, pc ? pc[29] : 0u, after[3]);
+    }
     return RPGPU_OK;
 }
 

@@ -1259,7 +1259,8 @@ RPC_HD int64_t decode_part(uint32_t kind, const uint8_t* in, uint64_t in_len, ui
 // The serial decoder's verdict for a planned body from its parts' decoded
 // sizes r(k) (-1: the part is corrupt): V_OK or V_ERROR with *len as the serial
 // decoder leaves it, or kSplitSerial when only the serial decoder can tell (a
-// non-final LZ4 block decoded short: the serial decoder would place the next
+// non-final LZ4 block decoded short in a frame without a content size, or
+// with one the blocks add up to: the serial decoder would place the next
 // block elsewhere).  The first corrupt part, in order, ends the serial decode:
 // an LZ4 block -> V_ERROR with no output (lz4f_uncompress: decompressionFailed;
 // independent blocks decode the same wherever they are placed), a snappy chunk
@@ -1267,7 +1268,7 @@ RPC_HD int64_t decode_part(uint32_t kind, const uint8_t* in, uint64_t in_len, ui
 constexpr int32_t kSplitSerial = -1;
 template <class R>
 RPC_HD int32_t split_result(uint32_t codec, const uint8_t* in, uint64_t n, uint32_t parts, R&& r, uint64_t* len) {
-    uint64_t o = 0;
+    uint64_t o = 0, tot = 0;  // tot: the serial decoder's output, wherever it places the blocks
     bool placed = true, bad = false;
     auto check = [&](uint32_t k, uint32_t kind, uint64_t, uint64_t, uint64_t out_off, uint64_t out_cap, uint32_t) {
         if (bad) return;
@@ -1279,6 +1280,7 @@ RPC_HD int32_t split_result(uint32_t codec, const uint8_t* in, uint64_t n, uint3
         }
         if (kind == kPartLz4Block && k + 1 < parts && (uint64_t)d != out_cap) placed = false;
         o = out_off + (uint64_t)d;
+        tot += (uint64_t)d;
     };
     if ((codec == 3 ? lz4f_split(in, n, parts, check) : snappy_java_split(in, n, parts, check)) != parts)
         return kSplitSerial;
@@ -1286,15 +1288,20 @@ RPC_HD int32_t split_result(uint32_t codec, const uint8_t* in, uint64_t n, uint3
         *len = o;
         return V_ERROR;
     }
-    if (!placed) return kSplitSerial;
-    *len = o;
     if (codec == 3) {
+        // independent blocks decode to the same bytes wherever they are placed, so
+        // the serial decoder's total is known without it: a frame whose content
+        // size it contradicts fails (frameSize_wrong) even when a short block left
+        // the parts misplaced -- C5's split fallbacks, two 1 MiB frames per step
+        // that the wave decoder took 41 ms to re-decode
         const Lz4Frame f = lz4f_header(in, n);
-        if (f.content != 0 && o != f.content) {  // frameSize_wrong
+        if (f.content != 0 && tot != f.content) {  // frameSize_wrong
             *len = 0;
             return V_ERROR;
         }
     }
+    if (!placed) return kSplitSerial;
+    *len = o;
     return V_OK;
 }
 

@@ -917,19 +917,31 @@ __global__ __launch_bounds__(64) void decomp_wave_kernel(
 }
 
 // The parts of split batches, one lane each (CODEC 3: LZ4 blocks, 2: snappy
-// chunks); every part writes only its own output range, so they run in any
-// order.  A batch whose slot does not fit the caller's buffer decodes nothing.
+// chunks, 0: both); every part writes only its own output range, so they run in
+// any order.  A batch whose slot does not fit the caller's buffer decodes nothing.
+#ifndef RPGPU_PARTS_ONE_LAUNCH
+#define RPGPU_PARTS_ONE_LAUNCH 1
+#endif
+#ifndef RPGPU_PART_SPREAD
+#define RPGPU_PART_SPREAD 1
+#endif
 template <uint32_t CODEC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_WAVES))) void part_kernel(
     const SplitPart* __restrict__ parts, const uint32_t* __restrict__ pcount, uint32_t pcap,
     const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data, const uint64_t* __restrict__ slot,
     const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base, uint8_t* __restrict__ out,
     uint64_t out_cap, int32_t* __restrict__ pres) {
-    const uint32_t half = pcap / 2, base = CODEC == 3 ? 0 : half;
-    const uint32_t cnt = *pcount < half ? *pcount : half;
-    const uint32_t lanes = gridDim.x * blockDim.x;
-    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < cnt; g += lanes) {
-        const SplitPart t = parts[base + g];
+    const uint32_t half = pcap / 2;
+    // CODEC 0: both lists in one launch, the snappy chunks (the longer parts) on the
+    // first lanes; pcount = counters 4, 5 (LZ4, snappy)
+    const uint32_t c3 = CODEC == 2 ? 0u : (pcount[0] < half ? pcount[0] : half);
+    const uint32_t c2 = CODEC == 3 ? 0u : (pcount[CODEC == 0 ? 1 : 0] < half ? pcount[CODEC == 0 ? 1 : 0] : half);
+    // RPGPU_PART_SPREAD lanes per part (one decodes): fewer decoding lanes per wave
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid % RPGPU_PART_SPREAD) return;
+    const uint32_t lanes = gridDim.x * blockDim.x / RPGPU_PART_SPREAD;
+    for (uint32_t g = tid / RPGPU_PART_SPREAD; g < c2 + c3; g += lanes) {
+        const SplitPart t = parts[g < c2 ? half + g : g - c2];
         if (t.kind == kSkipPart) continue;
         const uint64_t off = block_base[t.batch / kScanBlock] + local[t.batch];
         int32_t r = -2;
@@ -937,7 +949,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_
             const uint8_t* in = data + descs[t.batch].offset + kHeaderSize + t.in_off;
             r = (int32_t)rpcodec::decode_part(t.kind, in, t.in_len, out + off + kHeaderSize + t.out_off, t.out_cap, t.hdr);
         }
-        pres[base + g] = r;
+        pres[g < c2 ? half + g : g - c2] = r;
     }
 }
 
@@ -1168,6 +1180,15 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     // (failures join the LZ wave list).  With bodies split above 80 KiB the
     // main stream's lane launches got shorter and the snappy parts moved over
     // from the second stream, which the zstd wave decoder keeps the longer one.
+#if RPGPU_PARTS_ONE_LAUNCH
+    // both codecs' parts in one launch: their lanes (C5: 43,712 + 23,765) are resident
+    // at once, so the LZ4 blocks run beside the snappy chunks instead of before them
+    if (parts3 || parts2) {
+        const uint32_t pgrid = (part_cap(n) < 131072u ? part_cap(n) + 255 : 131072u + 255) / 256 * RPGPU_PART_SPREAD;
+        part_kernel<0><<<pgrid, 256, 0, s>>>(p.parts, p.counter + 4, part_cap(n), d_descs, d_data, p.slot, p.local,
+                                             p.block_sum, d_out, out_cap, p.pres);
+    }
+#else
     const uint32_t pgrid = (part_cap(n) / 2 < 65536u ? part_cap(n) / 2 + 255 : 65536u + 255) / 256;
     if (parts3)
         part_kernel<3><<<pgrid, 256, 0, s>>>(p.parts, p.counter + 4, part_cap(n), d_descs, d_data, p.slot, p.local,
@@ -1175,6 +1196,7 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     if (parts2)
         part_kernel<2><<<pgrid, 256, 0, s>>>(p.parts, p.counter + 5, part_cap(n), d_descs, d_data, p.slot, p.local,
                                              p.block_sum, d_out, out_cap, p.pres);
+#endif
     if (ds) {
         if ((e = hipEventRecord(ds->parts, s)) != hipSuccess) return e;
     }

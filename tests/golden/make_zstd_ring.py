@@ -6,8 +6,12 @@ each with one match whose offset reaches into the previous ring segment
 the ring has wrapped, read the previous segment right past the write
 position, where libzstd's over-long copies (ZSTD_wildcopy, ZSTD_overlapCopy8,
 ZSTD_safecopy near the ring's end) left bytes -- 40 small ones (lane decoder)
-and 4 of 400 blocks (wave decoder).  Made by tests/native/zstd_fuzz.cpp
---dump-ring / --dump-band (the engine's own zstd encoder pieces, predefined FSE tables);
+and 4 of 400 blocks (wave decoder); and (`span_*`) frames whose second
+ring segment opens with a match spanning the previous segment's end into the
+current one's start, its second part at a distance that is or is not below
+16 (libzstd's ZSTD_overlapCopy8) -- 60 of a grid plus 20 random ones.  Made by
+tests/native/zstd_fuzz.cpp --dump-ring / --dump-band / --dump-span (the
+engine's own zstd encoder pieces, predefined FSE tables);
 the expected outputs come from the oracle (libzstd 1.4.9 through
 stream_zstd::do_uncompress) at test time.  Writes tests/golden/zstd_ring.npz."""
 import subprocess
@@ -43,12 +47,21 @@ def main():
             n = int.from_bytes(raw[p:p + 4], "little")
             band.append(np.frombuffer(raw[p + 4:p + 4 + n], dtype=np.uint8))
             p += 4 + n
+        subprocess.run([str(exe), "--seed", "13", "--dump-span", "20"], cwd=tmp, check=True)
+        raw = (Path(tmp) / "span.bin").read_bytes()
+        span, p = [], 0
+        while p < len(raw):
+            n = int.from_bytes(raw[p:p + 4], "little")
+            span.append(np.frombuffer(raw[p + 4:p + 4 + n], dtype=np.uint8))
+            p += 4 + n
     lens = np.array([len(f) for f in frames], dtype=np.int64)
     blens = np.array([len(f) for f in band], dtype=np.int64)
+    slens = np.array([len(f) for f in span], dtype=np.int64)
     np.savez_compressed(ROOT / "tests" / "golden" / "zstd_ring.npz", data=np.concatenate(frames), lens=lens,
-                        cases=np.array(CASES, dtype=np.int64), band_data=np.concatenate(band), band_lens=blens)
+                        cases=np.array(CASES, dtype=np.int64), band_data=np.concatenate(band), band_lens=blens,
+                        span_data=np.concatenate(span), span_lens=slens)
     print("wrote", len(frames), "ring frames,", int(lens.sum()), "bytes;", len(band), "band frames,", int(blens.sum()),
-          "bytes")
+          "bytes;", len(span), "span frames,", int(slens.sum()), "bytes")
 
 
 if __name__ == "__main__":

@@ -707,7 +707,7 @@ Bytes span_frame(uint32_t lead, uint32_t ll, uint32_t len1, uint32_t m2) {
             seqs.push_back(rpzstdc::Seq{ll, ml, lw + len1});
             produced += ll + ml;
         } else {
-            for (int j = 0; j < 1000; j++) lits.push_back((uint8_t)('A' + (rng() % 16)));
+            for (int j = 0; j < 900; j++) lits.push_back((uint8_t)('A' + (rng() % 16)));
             seqs.push_back(rpzstdc::Seq{900, 24, 1 + (uint32_t)below(k == 0 ? 899 : 1000)});
             produced = 924;
         }
@@ -722,8 +722,9 @@ Bytes span_frame(uint32_t lead, uint32_t ll, uint32_t len1, uint32_t m2) {
     return f;
 }
 
-long n_span = 0;
+long n_span = 0, n_span_ok = 0;
 void check_span(long cases) {
+    const long ok0 = n_ok;
     for (uint32_t lead : {0u, 1u, 3u})
         for (uint32_t ll : {0u, 1u, 5u, 15u, 16u, 17u})
             for (uint32_t len1 : {1u, 2u, 7u, 8u, 9u, 15u, 16u, 17u, 40u})
@@ -735,6 +736,7 @@ void check_span(long cases) {
         compare(span_frame((uint32_t)below(5), (uint32_t)below(40), 1 + (uint32_t)below(100), 1 + (uint32_t)below(100)));
         n_span++;
     }
+    n_span_ok = n_ok - ok0;
 }
 
 void check_band(long cases) {
@@ -809,6 +811,27 @@ int main(int argc, char** argv) {
             fclose(fp);
             return 0;
         }
+        if (!strcmp(argv[a], "--dump-span")) {  // RANDOM: span frames (u32 length + bytes each) to span.bin
+            rng.seed(seed);
+            unsigned extra = 0;
+            if (sscanf(argv[a + 1], "%u", &extra) != 1) return 2;
+            std::vector<Bytes> fs;
+            for (uint32_t lead : {0u, 3u})
+                for (uint32_t ll : {0u, 16u, 17u})
+                    for (uint32_t len1 : {1u, 8u, 9u, 16u, 40u})
+                        for (uint32_t m2 : {1u, 16u}) fs.push_back(span_frame(lead, ll, len1, m2));
+            for (unsigned k = 0; k < extra; k++)
+                fs.push_back(span_frame((uint32_t)below(5), (uint32_t)below(40), 1 + (uint32_t)below(100),
+                                        1 + (uint32_t)below(100)));
+            FILE* fp = fopen("span.bin", "wb");
+            if (!fp) return 2;
+            for (const Bytes& f : fs) {
+                const uint32_t n = (uint32_t)f.size();
+                if (fwrite(&n, 4, 1, fp) != 1 || fwrite(f.data(), 1, n, fp) != n) return 2;
+            }
+            fclose(fp);
+            return 0;
+        }
         if (!strcmp(argv[a], "--dump-ring")) {  // OFF[,BLOCKS,BAD]: a crafted ring frame to ring.zst
             rng.seed(seed);
             unsigned off = 0, nb = 8, bad = 5;
@@ -853,6 +876,7 @@ int main(int argc, char** argv) {
     printf("zstd fuzz: %ld cases (%ld through the ring pass), %ld decoded, %ld rejected: engine == oracle\n",
            n_cases, n_ring, n_ok, n_rejected);
     printf("block-parallel path: %ld large frames planned, %ld decoded: == decoder\n", n_blk, n_blk_ok);
-    printf("span frames (a match across the ring segments' boundary near the segment start): %ld == libzstd\n", n_span);
+    printf("span frames (a match across the ring segments' boundary near the segment start): %ld == libzstd (%ld decoded)\n", n_span,
+           n_span_ok);
     return 0;
 }
