@@ -206,11 +206,15 @@ constexpr uint64_t kLaneMaxSlot = 256u << 10;
 #endif
 constexpr uint64_t kZstdLaneMaxSlot = RPGPU_ZSTD_LANE_MAX;  // zstd: its lane / wave boundary
 __device__ __forceinline__ uint64_t lane_max(uint32_t codec) { return codec == 4 ? kZstdLaneMaxSlot : kLaneMaxSlot; }
-// zstd frames above this content size leave the lane decoder even in a lane-sized slot
+// zstd frames above this content size leave the lane decoder even in a lane-sized slot:
+// 64 KiB, the least the block-parallel planner takes (plan_blocks: a frame of at most
+// kStage goes libzstd's single-pass way).  C4's frames hold exactly 64 KiB and stay on
+// the lanes; C5 80 -> 64 KiB: the zstd lanes' longest frames 80 -> 64 KiB (r6n)
 #ifndef RPGPU_ZSTD_BLK_MIN
-#define RPGPU_ZSTD_BLK_MIN (80u << 10)
+#define RPGPU_ZSTD_BLK_MIN (64u << 10)
 #endif
 constexpr uint64_t kZstdBlkMin = RPGPU_ZSTD_BLK_MIN;
+static_assert(kZstdBlkMin >= rpzstd::kStage, "the block-parallel planner takes no frame of kStage or less");
 // the first frame's content size when the block-parallel decoder could take the
 // frame (no checksum, no dictionary: plan_blocks' header conditions), else 0 --
 // a lane-sized checksummed frame stays on the lanes, not the wave decoder
@@ -651,8 +655,21 @@ __global__ __launch_bounds__(256) void zstd_ring_kernel(
 // (rpgpu_zblk.h).  Counters: [24..25] literal bytes, [26..27] records planned
 // (u64), [28] pool blocks reserved, [30..31] / [32..33] the literal / record
 // regions' offsets in the output buffer (after the lane workspaces).
+// E1 + E2 workspace: one lane's Huffman or FSE tables
+union ZbWs {
+    rpzstd::HufWs h;
+    rpzstd::SeqWs s;
+};
+// RPGPU_ZBLK_GWS 1: the entropy lanes' workspaces in the output buffer (HBM, after
+// the record region: [34..35] their offset, [36] their count), one lane per task
+// and every task at once; 0: in LDS, ~57 lanes per CU taking turns
+#ifndef RPGPU_ZBLK_GWS
+#define RPGPU_ZBLK_GWS 1
+#endif
+constexpr uint32_t kZbGwsLanes = 65536;
 __device__ __forceinline__ bool zb_fits(const uint32_t* counter, uint64_t out_cap) {
-    return cnt64(counter, 32) + (cnt64(counter, 26) + 16) * 8 <= out_cap;
+    return cnt64(counter, 32) + (cnt64(counter, 26) + 16) * 8 <= out_cap &&
+           cnt64(counter, 34) + (uint64_t)counter[36] * sizeof(ZbWs) <= out_cap;
 }
 
 // P: one lane per zstd wave list entry (the first kBlkFrames): the frame's
@@ -696,10 +713,6 @@ __global__ __launch_bounds__(256) void zblk_plan_kernel(
 
 // E1 + E2: one lane per task (block b's sequences: task b, its literals: task
 // used + b), each lane's Huffman / FSE workspace in LDS
-union ZbWs {
-    rpzstd::HufWs h;
-    rpzstd::SeqWs s;
-};
 __global__ __launch_bounds__(64) void zblk_entropy_kernel(
     const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data, const uint32_t* __restrict__ counter,
     const uint32_t* __restrict__ wlist, const ZbFrame* __restrict__ frames, rpzstd::Blk* __restrict__ pool,
@@ -720,6 +733,32 @@ __global__ __launch_bounds__(64) void zblk_entropy_kernel(
 #ifdef RPZB_DIAG_TASKS  // diagnostics build: 1 literals only, 2 sequences only (timing)
         if ((seq ? 2 : 1) != RPZB_DIAG_TASKS) continue;
 #endif
+        const ZbFrame f = frames[k];
+        const uint8_t* in = data + descs[wlist[k]].offset + kHeaderSize;
+        const uint32_t j = b - f.first;
+        if (seq)
+            pool[b].e2 = rpzstd::blk_sequences(in, pool + f.first, j, reinterpret_cast<uint64_t*>(out + roff) + f.recs, w.s);
+        else
+            pool[b].e1 = rpzstd::blk_literals(in, pool + f.first, j, out + loff + f.lits, w.h);
+    }
+}
+
+// E1 + E2 with the workspaces in HBM: one lane per task, all of them at once
+// (C5: 61,770 tasks), each lane's tables in its own 2,864-byte slot
+__global__ __launch_bounds__(256) void zblk_entropy_g_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data, const uint32_t* __restrict__ counter,
+    const uint32_t* __restrict__ wlist, const ZbFrame* __restrict__ frames, rpzstd::Blk* __restrict__ pool,
+    const uint32_t* __restrict__ bframe, uint8_t* __restrict__ out, uint64_t out_cap) {
+    const uint32_t wl = counter[36];
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= wl || !zb_fits(counter, out_cap)) return;
+    ZbWs& w = reinterpret_cast<ZbWs*>(out + cnt64(counter, 34))[tid];
+    const uint32_t used = counter[28] < kBlkPool ? counter[28] : kBlkPool;
+    const uint64_t loff = cnt64(counter, 30), roff = cnt64(counter, 32);
+    for (uint32_t t = tid; t < 2 * used; t += wl) {
+        const bool seq = t < used;
+        const uint32_t b = seq ? t : t - used, k = bframe[b];
+        if (k == ~0u) continue;
         const ZbFrame f = frames[k];
         const uint8_t* in = data + descs[wlist[k]].offset + kHeaderSize;
         const uint32_t j = b - f.first;
@@ -844,7 +883,14 @@ __global__ void decomp_ws_kernel(uint32_t* __restrict__ counter, uint32_t cap, u
     counter[32] = (uint32_t)br;
     counter[33] = (uint32_t)(br >> 32);
     const bool blk = counter[28] != 0;
-    if (out_bytes) *out_bytes = blk ? br + (cnt64(counter, 26) + 16) * 8 : ws_end;
+    // the entropy lanes' workspaces (RPGPU_ZBLK_GWS)
+    const uint64_t bw = (br + (cnt64(counter, 26) + 16) * 8 + 255) & ~(uint64_t)255;
+    const uint32_t used = counter[28] < kBlkPool ? counter[28] : kBlkPool;
+    const uint32_t wl = RPGPU_ZBLK_GWS ? (2 * used < kZbGwsLanes ? 2 * used : kZbGwsLanes) : 0u;
+    counter[34] = (uint32_t)bw;
+    counter[35] = (uint32_t)(bw >> 32);
+    counter[36] = wl;
+    if (out_bytes) *out_bytes = blk ? bw + (uint64_t)wl * sizeof(ZbWs) : ws_end;
 }
 
 // One batch body through the codec restatement, bytes produced by the wave.
@@ -1123,7 +1169,7 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     auto c64 = [&](int k) { return (uint64_t)pc[k] | ((uint64_t)pc[k + 1] << 32); };
     const bool parts3 = !pc || pc[4] != 0, parts2 = !pc || pc[5] != 0;
     const bool blk_any = !pc || pc[28] != 0;
-    const bool blk_fits = pc && c64(32) + (c64(26) + 16) * 8 <= out_cap;
+    const bool blk_fits = pc && c64(32) + (c64(26) + 16) * 8 <= out_cap && c64(34) + (uint64_t)pc[36] * sizeof(ZbWs) <= out_cap;
     const bool zwave_any = !pc || pc[2] > (blk_fits ? pc[29] : 0u);
     const bool lzwave_any = !pc || pc[6] != 0 || parts3 || parts2;  // split fallbacks join the LZ list
     const bool zlane_any = !pc || pc[7] != 0;
@@ -1211,9 +1257,16 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
             d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.counter + 1,
             p.lits, p.wlist, p.counter + 2, zb.frames, p.counter);
     if (blk_any) {
+#if RPGPU_ZBLK_GWS
+        // one lane per task: pc[36] of them when the plan's counts are here, else the most
+        const uint32_t wl = pc ? pc[36] : kZbGwsLanes;
+        zblk_entropy_g_kernel<<<(wl + 255) / 256, 256, 0, ws>>>(d_descs, d_data, p.counter, p.wlist, zb.frames, zb.pool,
+                                                               zb.bframe, d_out, out_cap);
+#else
         const ZbLaunch zq = zblk_launch();
         zblk_entropy_kernel<<<zq.grid, 64, zq.lanes * sizeof(ZbWs), ws>>>(d_descs, d_data, p.counter, p.wlist, zb.frames,
                                                                        zb.pool, zb.bframe, d_out, out_cap, zq.lanes);
+#endif
         if ((e = hipGetLastError()) != hipSuccess) return e;
         zblk_exec_kernel<<<zb_frames(n), 64, 0, ws>>>(d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
                                                       out_cap, d_out_descs, p.counter, p.wlist, zb.frames, zb.pool);
@@ -1234,13 +1287,19 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                                                                   nullptr, nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t lzb = (n + 255) / 256;
-    decomp_lane_kernel<3><<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
-                                              out_cap, d_out_descs, p.scount);
+    // RPGPU_LZ4_LANE_AUX 1: the LZ4 lanes on the second stream, behind its block-parallel
+    // zstd stages (once their entropy lanes left HBM workspaces, the shorter chain)
+#ifndef RPGPU_LZ4_LANE_AUX
+#define RPGPU_LZ4_LANE_AUX 1
+#endif
+    decomp_lane_kernel<3><<<lzb, 256, 0, RPGPU_LZ4_LANE_AUX ? ws : s>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
+                                                                        p.block_sum, d_dres, d_out, out_cap,
+                                                                        d_out_descs, p.scount);
     // the snappy lanes (second stream) start once the LZ4 lanes are done: both kernels'
     // 1,024 workgroups want the whole GPU, and racing them for it slowed C3's LZ4 lanes
     // (78 or 93 ms per step from run to run); in C5 the snappy lanes ran beside the zstd
     // lanes, after the LZ4 lanes, anyway
-    if (ds) {
+    if (ds && !RPGPU_LZ4_LANE_AUX) {
         if ((e = hipEventRecord(ds->lanes, s)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(ws, ds->lanes, 0)) != hipSuccess) return e;
     }

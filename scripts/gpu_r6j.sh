@@ -13,7 +13,12 @@ run() {  # tag, lib ('' = the library), args...
 }
 C5="--config c5 --steps 3 --warmup 1 --full-check 0"
 run base "" $C5
-for v in RPGPU_ZBLK_WAVES_4 RPGPU_ZBLK_WAVES_2 RPGPU_ZBLK_WAVES_4_RPGPU_ZSTD_BLK_MIN_32768 RPGPU_ZSTD_BLK_MIN_32768 RPGPU_ZBLK_WAVES_4; do
+for v in RPGPU_LZ4_LANE_AUX_1 RPGPU_ZSTD_BLK_MIN_65536 RPGPU_LZ4_LANE_AUX_1_RPGPU_ZSTD_BLK_MIN_65536; do
   run $v build/vx/librpgpu_$v.so $C5
 done
 run base2 "" $C5
+if [ -n "$TL_LIB" ]; then
+  export RPGPU_DIAG_LIB=$TL_LIB
+  timeout -k 10 300 rocprofv3 --kernel-trace -d $O/prof -o run -- python -u bench.py --no-cpu-baseline $C5 > $O/tl.json 2> $O/tl.err || { tail -5 $O/tl.err; exit 1; }
+  python scripts/timeline_db.py $(find $O/prof -name "*.db") 2 > $O/timeline.txt
+fi
