@@ -121,7 +121,8 @@ uint32_t part_cap(uint32_t n) { return 2 * ((n + 4096u) / 2); }
 struct Parts {
     uint64_t *slot, *local, *block_sum;
     uint32_t* wlist;   // wave-owned batches: zstd [0, n), LZ [n, 2n); zstd lane batches [2n, 3n) and
-                       // the ones whose ring wrapped behind them
+                       // the ones whose ring wrapped behind them; LZ4 lane batches from 4n up,
+                       // snappy lane batches from 5n - 1 down
     uint32_t *sfirst, *scount;  // a split batch's parts (scount 0: not split)
     SplitPart* parts;
     int32_t* pres;     // decoded size per part (-1 error, -2 no slot)
@@ -132,7 +133,7 @@ struct Parts {
 };
 size_t parts_head(uint32_t n) {
     const size_t nb = (n + kScanBlock - 1) / kScanBlock;
-    return ((size_t)n * 40 + nb * 8 + 255) & ~(size_t)255;  // slot, local: 8 B; wlist: 4 x 4 B; sfirst, scount
+    return ((size_t)n * 44 + nb * 8 + 255) & ~(size_t)255;  // slot, local: 8 B; wlist: 5 x 4 B; sfirst, scount
 }
 size_t counter_offset(uint32_t n) { return (parts_head(n) + validate_scratch_bytes(n) + 255) & ~(size_t)255; }
 size_t zws_offset(uint32_t n) { return counter_offset(n) + 256 + (size_t)decomp_waves(n) * kLitScratch; }
@@ -176,7 +177,7 @@ Parts parts(void* p, uint32_t n, uint32_t cap) {
     s.local = s.slot + n;
     s.block_sum = s.local + n;
     s.wlist = reinterpret_cast<uint32_t*>(s.block_sum + (n + kScanBlock - 1) / kScanBlock);
-    s.sfirst = s.wlist + 4 * (size_t)n;
+    s.sfirst = s.wlist + 5 * (size_t)n;
     s.scount = s.sfirst + n;
     s.vscratch = b + parts_head(n);
     s.counter = reinterpret_cast<uint32_t*>(b + counter_offset(n));
@@ -395,14 +396,24 @@ __global__ __launch_bounds__(kScanBlock) void decomp_caps_kernel(
         sfirst[i] = sf;
         scount[i] = sc;
     }
-    // lane batches of the snappy and gzip decoders (whose kernels walk every batch):
-    // counts only, so a run can skip a launch with nothing to do (counters 12, 13)
+    // lane batches of the snappy, LZ4 and gzip decoders: counted (counters 12, 14, 13),
+    // so a run can skip a launch with nothing to do, and the snappy / LZ4 ones listed
+    // for the LZ lane kernel (LZ4 from wlist[4n] up, snappy from wlist[5n - 1] down),
+    // one atomic per wave and list
     {
         const bool sl = i < n && wanted && codec == 2 && (over || sz <= lane_max(2)) && sc == 0;
+        const bool ll = i < n && wanted && codec == 3 && (over || sz <= lane_max(3)) && sc == 0;
         const bool gl = i < n && wanted && codec == 1;
-        const uint64_t sm = __ballot(sl), gm = __ballot(gl);
-        if (l == 0 && sm) atomicAdd(wcount + 10, (uint32_t)__builtin_popcountll(sm));
+        const uint64_t sm = __ballot(sl), lm = __ballot(ll), gm = __ballot(gl);
+        uint32_t sb = 0, lb = 0;
+        if (l == 0 && sm) sb = atomicAdd(wcount + 10, (uint32_t)__builtin_popcountll(sm));
+        if (l == 0 && lm) lb = atomicAdd(wcount + 12, (uint32_t)__builtin_popcountll(lm));
         if (l == 0 && gm) atomicAdd(wcount + 11, (uint32_t)__builtin_popcountll(gm));
+        sb = (uint32_t)__shfl(sb, 0, 64);
+        lb = (uint32_t)__shfl(lb, 0, 64);
+        const uint64_t below = (1ull << l) - 1;
+        if (sl) wlist[5 * (size_t)n - 1 - (sb + (uint32_t)__builtin_popcountll(sm & below))] = i;
+        if (ll) wlist[4 * (size_t)n + lb + (uint32_t)__builtin_popcountll(lm & below)] = i;
     }
     // zstd batches for the lane decoder (not wave-owned; overflowing ones too,
     // for their verdict): listed with one atomic per wave
@@ -549,6 +560,55 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_
         }
         finish_batch(i, reread(descs)[i], reread(vres)[i], off, sz, verdict, len, data, out, dres, out_descs);
     }
+}
+
+// The LZ4 and snappy lane batches in one launch, one lane each, from the plan's
+// lists (snappy first, then LZ4: waves of one codec, every lane busy -- the
+// per-codec kernels above walk every batch index and leave three lanes in four
+// idle on a mixed arena).  The batches nobody decodes get their verdict from
+// skip_kernel.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_WAVES))) void lz_lane_kernel(
+    const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
+    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
+    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
+    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
+    rpgpu_batch_desc* __restrict__ out_descs, const uint32_t* __restrict__ counter, const uint32_t* __restrict__ list) {
+    const uint32_t c2 = counter[12] < n ? counter[12] : n;
+    const uint32_t c3 = counter[14] < n - c2 ? counter[14] : n - c2;
+    const uint32_t lanes = gridDim.x * blockDim.x;
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < c2 + c3; g += lanes) {
+        const uint32_t i = g < c2 ? list[n - 1 - g] : list[g - c2];
+        uint64_t sz = slot[i];
+        const uint64_t off = block_base[i / kScanBlock] + local[i];
+        int32_t verdict = RPGPU_V_SKIPPED;
+        uint64_t len = 0;
+        {
+            const rpgpu_batch_desc d = descs[i];
+            const rpgpu_batch_result v = vres[i];
+            if (plan_slot(sz, off, out_cap, verdict, len)) {
+                rpcodec::LaneEmit em;  // LZ4 blocks: lz4_block_lane
+                verdict = rpcodec::uncompress(em, v.codec, data + d.offset + kHeaderSize, body_len(v),
+                                              out + off + kHeaderSize, sz - kHeaderSize - rpcodec::kSlack, &len);
+            }
+        }
+        finish_batch(i, reread(descs)[i], reread(vres)[i], off, sz, verdict, len, data, out, dres, out_descs);
+    }
+}
+// the verdict (SKIPPED) of every batch the decompression does not take
+__global__ __launch_bounds__(256) void skip_kernel(const rpgpu_batch_desc* __restrict__ descs, uint32_t n,
+                                                   const uint8_t* __restrict__ data,
+                                                   const rpgpu_batch_result* __restrict__ vres,
+                                                   const uint64_t* __restrict__ slot, const uint64_t* __restrict__ local,
+                                                   const uint64_t* __restrict__ block_base,
+                                                   rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out,
+                                                   rpgpu_batch_desc* __restrict__ out_descs) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const rpgpu_batch_desc d = descs[i];
+    const rpgpu_batch_result v = vres[i];
+    if (decomp_wanted(d, v)) return;
+    finish_batch(i, d, v, block_base[i / kScanBlock] + local[i], slot[i], RPGPU_V_SKIPPED, 0, data, out, dres,
+                 out_descs);
 }
 
 // zstd batches up to kLaneMaxSlot (FAM 4) / all gzip batches (FAM 1): one lane
@@ -1133,7 +1193,7 @@ hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const
     // counters 2, 3: wave list lengths; 4, 5: LZ4 / snappy parts; 7: zstd lane list
     if ((e = hipMemsetAsync(p.counter + 2, 0, 4 * sizeof(uint32_t), s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(p.counter + 7, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(p.counter + 12, 0, 2 * sizeof(uint32_t), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(p.counter + 12, 0, 3 * sizeof(uint32_t), s)) != hipSuccess) return e;
     decomp_caps_kernel<<<nb, kScanBlock, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
                                                  max_decoded, p.counter + 2, p.wlist, p.sfirst, p.scount, p.parts,
                                                  part_cap(n));
@@ -1287,6 +1347,24 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                                                                   nullptr, nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t lzb = (n + 255) / 256;
+    // RPGPU_LZ_LANE_LIST 1: the LZ4 and snappy lane batches in one launch from the plan's
+    // lists (lz_lane_kernel) on the second stream, behind its block-parallel zstd stages;
+    // the undecoded batches' verdicts on the main stream (skip_kernel).  0: one kernel
+    // per codec over every batch index (decomp_lane_kernel), as in round 5.
+#ifndef RPGPU_LZ_LANE_LIST
+#define RPGPU_LZ_LANE_LIST 1
+#endif
+#if RPGPU_LZ_LANE_LIST
+    skip_kernel<<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, d_out_descs);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (!pc || pc[12] + pc[14] != 0) {
+        const uint32_t cnt = pc ? pc[12] + pc[14] : n;
+        lz_lane_kernel<<<(cnt + 255) / 256, 256, 0, ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
+                                                          d_dres, d_out, out_cap, d_out_descs, p.counter,
+                                                          p.wlist + 4 * (size_t)n);
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+#else
     // RPGPU_LZ4_LANE_AUX 1: the LZ4 lanes on the second stream, behind its block-parallel
     // zstd stages (once their entropy lanes left HBM workspaces, the shorter chain)
 #ifndef RPGPU_LZ4_LANE_AUX
@@ -1312,6 +1390,7 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
         decomp_lane_kernel<2><<<lzb, 256, 0, RPGPU_SNAPPY_LANE_AUX ? ws : s>>>(
             d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.scount);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+#endif
 #if !RPGPU_ZSTD_LANE_STREAM
     if ((e = zlanes()) != hipSuccess) return e;
 #else
