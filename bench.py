@@ -620,8 +620,10 @@ def main() -> int:
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": None,
-                     "kernel": ("pipeline: validate_kernel + decomp_caps_kernel + decomp_kernel / "
-                                "zstd_kernel + validate_kernel, walk_kernel over the rewritten batches"
+                     "kernel": ("pipeline: validate_kernel + walk_kernel, the decompress plan "
+                                "(decomp_caps_kernel, zblk_plan_kernel), the decoders (part_kernel, "
+                                "lz_lane_kernel, ws_lane_kernel, zblk_entropy_g_kernel + zblk_exec_kernel, "
+                                "wave decoders) and validate_kernel + walk_kernel over the rewritten batches"
                                 if decompress else "validate_kernel + walk_kernel"),
                      "kernel_ms": round(run_ms, 4),
                      "algorithmic_bytes_per_launch": int(alg_bytes)},
