@@ -144,6 +144,13 @@ size_t parts_offset(uint32_t n, uint32_t cap) {
 // parts: per zstd wave list entry (the first kBlkFrames) its
 // frame record, then a pool of kBlkPool blocks and each block's entry
 constexpr uint32_t kBlkFrames = 16384, kBlkPool = 65536;
+// the pool's blocks for an arena of n batches: no more than n frames of kBlkMax blocks
+// can be planned (a scratch for n = 1 no longer carries 4.4 MB of pool);
+// the plan leaves it in counter[37] for the kernels
+uint32_t blk_pool(uint32_t n) {
+    const uint64_t c = (uint64_t)(n ? n : 1) * rpzstd::kBlkMax;
+    return c < kBlkPool ? (uint32_t)c : kBlkPool;
+}
 struct ZbFrame {
     uint32_t first, nblk;  // pool blocks; nblk 0: not planned (the wave decoder's)
     uint64_t lits, recs;   // offsets in the literal / record regions
@@ -155,7 +162,7 @@ size_t zblk_offset(uint32_t n, uint32_t cap) {
     return (parts_offset(n, cap) + (size_t)part_cap(n) * (sizeof(SplitPart) + sizeof(int32_t)) + 255) & ~(size_t)255;
 }
 size_t zblk_bytes(uint32_t n) {
-    return (size_t)zb_frames(n) * sizeof(ZbFrame) + (size_t)kBlkPool * (sizeof(rpzstd::Blk) + 4) + 256;
+    return (size_t)zb_frames(n) * sizeof(ZbFrame) + (size_t)blk_pool(n) * (sizeof(rpzstd::Blk) + 4) + 256;
 }
 struct ZbParts {
     ZbFrame* frames;
@@ -166,7 +173,7 @@ ZbParts zbparts(void* p, uint32_t n, uint32_t cap) {
     uint8_t* b = static_cast<uint8_t*>(p) + zblk_offset(n, cap);
     ZbParts z;
     z.pool = reinterpret_cast<rpzstd::Blk*>(b);
-    z.frames = reinterpret_cast<ZbFrame*>(z.pool + kBlkPool);
+    z.frames = reinterpret_cast<ZbFrame*>(z.pool + blk_pool(n));
     z.bframe = reinterpret_cast<uint32_t*>(z.frames + zb_frames(n));
     return z;
 }
@@ -714,7 +721,8 @@ __global__ __launch_bounds__(256) void zstd_ring_kernel(
 // ------------------------------------------- block-parallel zstd (large frames)
 // (rpgpu_zblk.h).  Counters: [24..25] literal bytes, [26..27] records planned
 // (u64), [28] pool blocks reserved, [30..31] / [32..33] the literal / record
-// regions' offsets in the output buffer (after the lane workspaces).
+// regions' offsets in the output buffer (after the lane workspaces), [37] the
+// pool's capacity.
 // E1 + E2 workspace: one lane's Huffman or FSE tables
 union ZbWs {
     rpzstd::HufWs h;
@@ -752,7 +760,7 @@ __global__ __launch_bounds__(256) void zblk_plan_kernel(
         const rpzstd::BlkPlan pl = rpzstd::plan_blocks(in, body_len(v), cap, nullptr);
         if (pl.ok && pl.nblk > 0) {
             const uint32_t first = atomicAdd(counter + 28, pl.nblk);
-            if ((uint64_t)first + pl.nblk <= kBlkPool) {
+            if ((uint64_t)first + pl.nblk <= counter[37]) {
                 f.first = first;
                 f.nblk = pl.nblk;
                 f.lits = atomicAdd(reinterpret_cast<unsigned long long*>(counter + 24), (unsigned long long)pl.lits);
@@ -764,7 +772,7 @@ __global__ __launch_bounds__(256) void zblk_plan_kernel(
                 rpzstd::plan_blocks(in, body_len(v), cap, pool + first);
                 for (uint32_t j = 0; j < pl.nblk; j++) bframe[first + j] = k;
             } else {
-                for (uint32_t j = first; j < kBlkPool; j++) bframe[j] = ~0u;  // a hole: no entry's
+                for (uint32_t j = first; j < counter[37]; j++) bframe[j] = ~0u;  // a hole: no entry's
             }
         }
     }
@@ -781,7 +789,7 @@ __global__ __launch_bounds__(64) void zblk_entropy_kernel(
     const uint32_t l = threadIdx.x;
     if (l >= per_wg || !zb_fits(counter, out_cap)) return;
     ZbWs& w = reinterpret_cast<ZbWs*>(dyn_lds)[l];
-    const uint32_t used = counter[28] < kBlkPool ? counter[28] : kBlkPool;
+    const uint32_t used = counter[28] < counter[37] ? counter[28] : counter[37];
     const uint64_t loff = cnt64(counter, 30), roff = cnt64(counter, 32);
     const uint32_t lanes = gridDim.x * per_wg;
     // tasks [0, used): the blocks' sequences (the longer ones), then [used, 2 used) their
@@ -813,7 +821,7 @@ __global__ __launch_bounds__(256) void zblk_entropy_g_kernel(
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     if (tid >= wl || !zb_fits(counter, out_cap)) return;
     ZbWs& w = reinterpret_cast<ZbWs*>(out + cnt64(counter, 34))[tid];
-    const uint32_t used = counter[28] < kBlkPool ? counter[28] : kBlkPool;
+    const uint32_t used = counter[28] < counter[37] ? counter[28] : counter[37];
     const uint64_t loff = cnt64(counter, 30), roff = cnt64(counter, 32);
     for (uint32_t t = tid; t < 2 * used; t += wl) {
         const bool seq = t < used;
@@ -945,7 +953,7 @@ __global__ void decomp_ws_kernel(uint32_t* __restrict__ counter, uint32_t cap, u
     const bool blk = counter[28] != 0;
     // the entropy lanes' workspaces (RPGPU_ZBLK_GWS)
     const uint64_t bw = (br + (cnt64(counter, 26) + 16) * 8 + 255) & ~(uint64_t)255;
-    const uint32_t used = counter[28] < kBlkPool ? counter[28] : kBlkPool;
+    const uint32_t used = counter[28] < counter[37] ? counter[28] : counter[37];
     const uint32_t wl = RPGPU_ZBLK_GWS ? (2 * used < kZbGwsLanes ? 2 * used : kZbGwsLanes) : 0u;
     counter[34] = (uint32_t)bw;
     counter[35] = (uint32_t)(bw >> 32);
@@ -1137,7 +1145,7 @@ __global__ __launch_bounds__(64) void uncompress_one_kernel(uint32_t codec, cons
 // zstd / LZ wave list lengths, 4 / 5 LZ4 / snappy parts, 6 the plan's LZ list
 // length.  A run appends split fallbacks to the LZ list, so each run starts
 // from the plan's length (a plan may be run any number of times).
-__global__ void decomp_counters_kernel(uint32_t* c, uint32_t run) {
+__global__ void decomp_counters_kernel(uint32_t* c, uint32_t run, uint32_t pool_cap) {
     if (threadIdx.x != 0) return;
     if (run) {
         c[0] = 0;
@@ -1146,6 +1154,7 @@ __global__ void decomp_counters_kernel(uint32_t* c, uint32_t run) {
         c[11] = 0;  // zstd lane batches whose ring wrapped
     } else {
         c[6] = c[3];
+        c[37] = pool_cap;  // the block pool's capacity (blk_pool)
     }
 }
 
@@ -1199,7 +1208,7 @@ hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const
                                                  part_cap(n));
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    decomp_counters_kernel<<<1, 64, 0, s>>>(p.counter, 0);
+    decomp_counters_kernel<<<1, 64, 0, s>>>(p.counter, 0, blk_pool(n));
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // the block-parallel decoder's frames among the zstd wave list (counters 24..29)
     if ((e = hipMemsetAsync(p.counter + 24, 0, 6 * sizeof(uint32_t), s)) != hipSuccess) return e;
@@ -1235,7 +1244,7 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     const bool zlane_any = !pc || pc[7] != 0;
     const bool snappy_any = !pc || pc[12] != 0, gzip_any = !pc || pc[13] != 0;
     const uint32_t nblk = (n + 255) / 256;
-    decomp_counters_kernel<<<1, 64, 0, s>>>(p.counter, 1);
+    decomp_counters_kernel<<<1, 64, 0, s>>>(p.counter, 1, 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // large batches on the wave decoders, on a second stream beside the lanes;
