@@ -202,12 +202,14 @@ size_t decomp_counter_offset(uint32_t n, uint32_t) { return counter_offset(n); }
 // slots above this go to the wave decoders (a lane's serial decode of a
 // large body would hold up the whole launch)
 constexpr uint64_t kLaneMaxSlot = 256u << 10;
-// RPGPU_ZSTD_LANE_STREAM 1: the zstd / gzip lane decoders on a third stream,
-// launched first (measured: C5 265.7 vs 236.5 ms -- with GPU_MAX_HW_QUEUES 4 the
-// third stream shares a hardware queue with the main one, so its kernels run
-// before the main stream's instead of beside them; profiles/r5/NOTES.md r5s)
+// RPGPU_ZSTD_LANE_STREAM: the zstd / gzip lane decoders on the main stream after the
+// LZ lanes (0), on a third stream launched first (1: aux2; round 5 measured C5 265.7 vs
+// 236.5 ms, profiles/r5/NOTES.md r5s), or (2, the default since round 6) on the walk
+// overlap's stream, idle during decompression, with the LZ lanes moved to the main
+// stream behind the part kernel: C5 146.7 / 149.1 -> 139.8 / 141.8 ms, C4 and C3
+// unchanged (profiles/r6/NOTES.md r6t)
 #ifndef RPGPU_ZSTD_LANE_STREAM
-#define RPGPU_ZSTD_LANE_STREAM 0
+#define RPGPU_ZSTD_LANE_STREAM 2
 #endif
 #ifndef RPGPU_ZSTD_LANE_MAX
 #define RPGPU_ZSTD_LANE_MAX (256u << 10)
@@ -1250,14 +1252,18 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     // large batches on the wave decoders, on a second stream beside the lanes;
     // the zstd / gzip lane decoders on a third (RPGPU_ZSTD_LANE_STREAM 0: on the
     // main stream after the LZ4 / snappy lanes, as before round 5)
-    hipStream_t ws = s, zs = s;
+    hipStream_t ws = s, zs = s, z2 = nullptr;
+    (void)z2;
     if (ds) {
         if ((e = hipEventRecord(ds->fork, s)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(ds->aux, ds->fork, 0)) != hipSuccess) return e;
         ws = ds->aux;
 #if RPGPU_ZSTD_LANE_STREAM
-        if ((e = hipStreamWaitEvent(ds->aux2, ds->fork, 0)) != hipSuccess) return e;
-        zs = ds->aux2;
+        // 2: the walk overlap's stream (idle during decompression, a hardware queue of
+        // its own) instead of aux2
+        z2 = (RPGPU_ZSTD_LANE_STREAM == 2 && ov) ? ov->aux : ds->aux2;
+        if ((e = hipStreamWaitEvent(z2, ds->fork, 0)) != hipSuccess) return e;
+        zs = z2;
 #endif
     }
     // the zstd / gzip lane decoders (on zs)
@@ -1357,8 +1363,9 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t lzb = (n + 255) / 256;
     // RPGPU_LZ_LANE_LIST 1: the LZ4 and snappy lane batches in one launch from the plan's
-    // lists (lz_lane_kernel) on the second stream, behind its block-parallel zstd stages;
-    // the undecoded batches' verdicts on the main stream (skip_kernel).  0: one kernel
+    // lists (lz_lane_kernel) on the main stream behind the part kernel (RPGPU_LZ_LANE_MAIN;
+    // else on the second, behind its block-parallel zstd stages); the undecoded batches'
+    // verdicts on the main stream (skip_kernel).  0: one kernel
     // per codec over every batch index (decomp_lane_kernel), as in round 5.
 #ifndef RPGPU_LZ_LANE_LIST
 #define RPGPU_LZ_LANE_LIST 1
@@ -1368,7 +1375,10 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (!pc || pc[12] + pc[14] != 0) {
         const uint32_t cnt = pc ? pc[12] + pc[14] : n;
-        lz_lane_kernel<<<(cnt + 255) / 256, 256, 0, ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
+#ifndef RPGPU_LZ_LANE_MAIN
+#define RPGPU_LZ_LANE_MAIN (RPGPU_ZSTD_LANE_STREAM != 0)
+#endif
+        lz_lane_kernel<<<(cnt + 255) / 256, 256, 0, RPGPU_LZ_LANE_MAIN ? s : ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
                                                           d_dres, d_out, out_cap, d_out_descs, p.counter,
                                                           p.wlist + 4 * (size_t)n);
     }
@@ -1409,7 +1419,7 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
         if ((e = hipEventRecord(ds->join, ds->aux)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(s, ds->join, 0)) != hipSuccess) return e;
 #if RPGPU_ZSTD_LANE_STREAM
-        if ((e = hipEventRecord(ds->join2, ds->aux2)) != hipSuccess) return e;
+        if ((e = hipEventRecord(ds->join2, z2)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(s, ds->join2, 0)) != hipSuccess) return e;
 #endif
     }
