@@ -245,7 +245,14 @@ rpgpu_ctx* rpgpu_open(int device, const rpgpu_opts* opts) {
     c->overlap.chunks = 16;
     if (opts && opts->walk_chunks >= 1 && opts->walk_chunks <= rpgpu::kMaxRunChunks) c->overlap.chunks = opts->walk_chunks;
     c->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
-    c->have_dstreams = hipStreamCreateWithFlags(&c->dstreams.aux, hipStreamNonBlocking) == hipSuccess &&
+    // RPGPU_AUX_PRIORITY 1 (default): the decompression's second stream -- the block-parallel
+    // zstd stages, the longest chain since round 6 -- at the main stream's priority
+    // (C5 129.0 / 129.2 -> 127.0 / 125.1 ms, profiles/r6/NOTES.md r6v)
+#ifndef RPGPU_AUX_PRIORITY
+#define RPGPU_AUX_PRIORITY 1
+#endif
+    c->have_dstreams = (RPGPU_AUX_PRIORITY ? hipStreamCreateWithPriority(&c->dstreams.aux, hipStreamNonBlocking, prio_hi)
+                                           : hipStreamCreateWithFlags(&c->dstreams.aux, hipStreamNonBlocking)) == hipSuccess &&
                        hipStreamCreateWithFlags(&c->dstreams.aux2, hipStreamNonBlocking) == hipSuccess &&
                        hipEventCreateWithFlags(&c->dstreams.fork, hipEventDisableTiming) == hipSuccess &&
                        hipEventCreateWithFlags(&c->dstreams.join, hipEventDisableTiming) == hipSuccess &&

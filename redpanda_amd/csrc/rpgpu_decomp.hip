@@ -205,9 +205,9 @@ constexpr uint64_t kLaneMaxSlot = 256u << 10;
 // RPGPU_ZSTD_LANE_STREAM: the zstd / gzip lane decoders on the main stream after the
 // LZ lanes (0), on a third stream launched first (1: aux2; round 5 measured C5 265.7 vs
 // 236.5 ms, profiles/r5/NOTES.md r5s), or (2, the default since round 6) on the walk
-// overlap's stream, idle during decompression, with the LZ lanes moved to the main
-// stream behind the part kernel: C5 146.7 / 149.1 -> 139.8 / 141.8 ms, C4 and C3
-// unchanged (profiles/r6/NOTES.md r6t)
+// overlap's stream, idle during decompression and a hardware queue of its own, with the
+// LZ lanes behind them there (RPGPU_LZ_LANE_MAIN 2): C5 146.7 / 149.1 -> 129.2 / 129.0
+// ms, C4 and C3 unchanged (profiles/r6/NOTES.md r6t, r6u)
 #ifndef RPGPU_ZSTD_LANE_STREAM
 #define RPGPU_ZSTD_LANE_STREAM 2
 #endif
@@ -1363,9 +1363,10 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t lzb = (n + 255) / 256;
     // RPGPU_LZ_LANE_LIST 1: the LZ4 and snappy lane batches in one launch from the plan's
-    // lists (lz_lane_kernel) on the main stream behind the part kernel (RPGPU_LZ_LANE_MAIN;
-    // else on the second, behind its block-parallel zstd stages); the undecoded batches'
-    // verdicts on the main stream (skip_kernel).  0: one kernel
+    // lists (lz_lane_kernel) behind the zstd lanes on the third stream (RPGPU_LZ_LANE_MAIN
+    // 2; 1: on the main stream behind the parts, 0: on the second behind the block-parallel
+    // zstd stages); the undecoded batches' verdicts on the main stream (skip_kernel).
+    // 0: one kernel
     // per codec over every batch index (decomp_lane_kernel), as in round 5.
 #ifndef RPGPU_LZ_LANE_LIST
 #define RPGPU_LZ_LANE_LIST 1
@@ -1376,9 +1377,9 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     if (!pc || pc[12] + pc[14] != 0) {
         const uint32_t cnt = pc ? pc[12] + pc[14] : n;
 #ifndef RPGPU_LZ_LANE_MAIN
-#define RPGPU_LZ_LANE_MAIN (RPGPU_ZSTD_LANE_STREAM != 0)
+#define RPGPU_LZ_LANE_MAIN (RPGPU_ZSTD_LANE_STREAM != 0 ? 2 : 0)
 #endif
-        lz_lane_kernel<<<(cnt + 255) / 256, 256, 0, RPGPU_LZ_LANE_MAIN ? s : ws>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
+        lz_lane_kernel<<<(cnt + 255) / 256, 256, 0, RPGPU_LZ_LANE_MAIN == 2 ? zs : (RPGPU_LZ_LANE_MAIN ? s : ws)>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum,
                                                           d_dres, d_out, out_cap, d_out_descs, p.counter,
                                                           p.wlist + 4 * (size_t)n);
     }
