@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/r6final
+O=gpurun_out/${OUTTAG:-r6final}
 mkdir -p $O
 python -c "from redpanda_amd import engine; print('lib', engine.library_hash())"
 run() {  # name, limit, args
@@ -12,5 +12,5 @@ run() {  # name, limit, args
 }
 run c2 300 "--config c2" && run c1 300 "--config c1" && run c3 500 "--config c3 --steps 5 --warmup 2 --full-check 1" \
   && run c5 500 "--config c5 --steps 5 --warmup 2" && run c4 500 "--config c4 --steps 3 --warmup 1" || exit 1
-CFG=c2 TAG=r6final/prof STEPS=10 LIMIT=300 bash scripts/gpu_prof.sh || exit 1
-for c in c3 c5 c4; do CFG=$c TAG=r6final/prof STEPS=2 LIMIT=400 BENCH_ARGS="--full-check 0" bash scripts/gpu_prof.sh || exit 1; done
+CFG=c2 TAG=${OUTTAG:-r6final}/prof STEPS=10 LIMIT=300 bash scripts/gpu_prof.sh || exit 1
+for c in c3 c5 c4; do CFG=$c TAG=${OUTTAG:-r6final}/prof STEPS=2 LIMIT=400 BENCH_ARGS="--full-check 0" bash scripts/gpu_prof.sh || exit 1; done
