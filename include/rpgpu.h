@@ -421,12 +421,15 @@ typedef struct rpgpu_decomp_result {
 /* Scratch of the decompress path: the plan's slots, lists and scans, the
  * validation scratch of the rewritten batches, the wave decoders' literal
  * buffers, one 2 KB gzip workspace per gzip lane (min(n, 32768), fewer with
- * rpgpu_opts.decomp_ws_lanes, see rpgpu_decomp_scratch_bytes_ctx) and the part
- * list of split bodies (36 B per part, n + 4096 parts).  The zstd lane
- * workspaces (~19 KB each) are not in it: the plan counts the arena's zstd
- * batches and puts one workspace per batch (at most 131,072, or
- * decomp_ws_lanes) after the output slots, so an arena without zstd batches
- * reserves none (ABI 4). */
+ * rpgpu_opts.decomp_ws_lanes, see rpgpu_decomp_scratch_bytes_ctx), the part
+ * list of split bodies (36 B per part, n + 4096 parts) and the block-parallel
+ * zstd plan (48 B per frame for min(n, 16384) frames, 68 B per block for
+ * min(64 n, 65536) blocks).  The zstd lane workspaces (~19 KB each) are not in
+ * it: the plan counts the arena's zstd batches and puts one workspace per batch
+ * (at most 131,072, or decomp_ws_lanes) after the output slots, so an arena
+ * without zstd batches reserves none (ABI 4); nor are the block-parallel
+ * decoder's literal, record and entropy-workspace regions, which follow them
+ * when the plan takes frames. */
 size_t rpgpu_decomp_scratch_bytes(uint32_t n);
 /* The same for a context's rpgpu_opts.decomp_ws_lanes (never more than
  * rpgpu_decomp_scratch_bytes(n)); the scratch of a context's decompress calls
@@ -434,7 +437,9 @@ size_t rpgpu_decomp_scratch_bytes(uint32_t n);
 size_t rpgpu_decomp_scratch_bytes_ctx(const rpgpu_ctx* ctx, uint32_t n);
 /* Plan: per-batch output slots and their exclusive scan into d_scratch;
  * *d_out_bytes = output bytes needed: the slots, then (256-byte aligned) the
- * zstd lane workspaces.  The output buffer must hold *d_out_bytes +
+ * zstd lane workspaces, then, when large zstd frames are planned block by
+ * block, their literal and sequence-record regions and one 2,864-byte entropy
+ * workspace per task.  The output buffer must hold *d_out_bytes +
  * RPGPU_ARENA_TAIL_PAD bytes; with less, batches whose slot does not fit get
  * RPGPU_V_DECOMP_OVERFLOW, and so do the zstd lane batches when the
  * workspaces do not fit. */

@@ -98,3 +98,17 @@ def test_kafka_error_code_map(built):
         for size, mx in ((1000, 0), (1000, 999), (1000, 1000), (1 << 20, 1 << 20)):
             r["verdict"], r["size_bytes"] = v, size
             assert engine.Engine.kafka_error_code(r, mx) == reference_code(v, size, mx), (abi.VERDICT_NAMES[v], size, mx)
+
+
+def test_decomp_scratch_scales_with_the_arena(built):
+    """the block-parallel zstd pool is sized for the arena (at most 64
+    blocks per frame, one frame per batch), so a one-batch decompress no longer
+    reserves the 65,536-block pool (4.4 MB); the scratch grows with n and
+    stays below the whole-arena layouts' sum (no device needed)."""
+    from redpanda_amd import abi
+
+    f = abi.lib().rpgpu_decomp_scratch_bytes
+    assert f(1) < 1 << 20
+    sizes = [f(n) for n in (1, 16, 1024, 65536, 131072)]
+    assert sizes == sorted(sizes)
+    assert f(131072) < 1 << 30
