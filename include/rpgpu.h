@@ -447,7 +447,10 @@ int32_t rpgpu_decomp_plan_device(rpgpu_ctx* ctx, const rpgpu_batch_desc* d_descs
                                  const uint8_t* d_data, const rpgpu_batch_result* d_results,
                                  uint64_t* d_out_bytes, void* d_scratch, void* hip_stream);
 /* Run (needs the plan, same d_scratch): decode, rewrite, then validate, walk
- * and index the rewritten batches.  d_out_descs[i] / d_out_results[i]
+ * and index the rewritten batches.  The decoders fork from hip_stream onto the
+ * context's own streams and join back: issue a context's
+ * runs on one stream (or order them with events), never on two at once.
+ * d_out_descs[i] / d_out_results[i]
  * describe rewritten batch i (length 0, ops 0, verdict STREAM_SHORT where
  * nothing was decompressed); index entries are laid out as by
  * rpgpu_run_device over d_out_descs; *d_index_used = entries reserved. */
