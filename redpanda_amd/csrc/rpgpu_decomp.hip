@@ -17,12 +17,16 @@
 //                        read off the frame's block headers / chunk
 //                        preambles (gzip: the counted size) + kSlack;
 //                        exclusive scan of the slots
-//   decomp_lane_kernel / ws_lane_kernel
-//                        batches up to kLaneMaxSlot (gzip: all of them): one
-//                        lane per batch runs the codec restatement with direct
-//                        copies; 64 batches per wave keep the serial decode
-//                        SIMD-efficient
-//   decomp_wave_kernel   larger batches, concurrently on a second stream:
+//   part_kernel          LZ4 blocks / snappy-java chunks of large bodies with a
+//                        split plan, one lane per part; split_finish_kernel
+//                        turns the parts' sizes into the serial verdict
+//   lz_lane_kernel / ws_lane_kernel
+//                        batches up to kLaneMaxSlot (gzip: all of them), from
+//                        the plan's lists: one lane per batch runs the codec
+//                        restatement; skip_kernel writes the verdict of the
+//                        batches nothing decodes
+//   zblk_*_kernel        large zstd frames block-parallel (rpgpu_zblk.h)
+//   decomp_wave_kernel   larger batches without a plan, on a second stream:
 //                        one wavefront per batch (batches taken from an
 //                        atomic counter), the decisions uniform in all lanes,
 //                        the bytes produced by the wave 64 sequences at a
@@ -522,14 +526,11 @@ __device__ __forceinline__ bool wave_owned(const rpgpu_batch_desc& d, const rpgp
     return decomp_wanted(d, v) && !(sz & kOverCeiling) && sz > lane_max(v.codec) && (v.codec >= 2 && v.codec <= 4);
 }
 
-// LZ4 (CODEC 3, which also writes the verdict of every batch nobody decodes)
-// or snappy (CODEC 2) batches up to kLaneMaxSlot, one lane each; one instance
-// per codec keeps each at its own register count.  Lanes in flight bound these
-// latency-bound decodes: at <= 128 VGPRs (4 waves per SIMD) a C3-sized arena's
-// lanes are all resident at once.  LZ4 blocks take rpcodec::lz4_block_lane
-// (one memory round trip per sequence).  The descriptor and validation result
-// are read again after the decode (reread()) instead of being held in
-// registers across it.
+// Lane decoders run <= 128 VGPRs (4 waves per SIMD): a C3-sized arena's lanes
+// are all resident at once.  LZ4 blocks take rpcodec::lz4_block_lane (one
+// memory round trip per sequence).  The descriptor and validation result are
+// read again after the decode (reread()) instead of being held in registers
+// across it.
 #ifndef RPGPU_LANE_WAVES
 #define RPGPU_LANE_WAVES 4
 #endif
@@ -538,37 +539,6 @@ __device__ __forceinline__ const T* reread(const T* p) {  // the compiler may no
     uint64_t x = (uint64_t)p;
     asm volatile("" : "+s"(x));
     return reinterpret_cast<const T*>(x);
-}
-template <uint32_t CODEC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_WAVES))) void decomp_lane_kernel(
-    const rpgpu_batch_desc* __restrict__ descs, uint32_t n, const uint8_t* __restrict__ data,
-    const rpgpu_batch_result* __restrict__ vres, const uint64_t* __restrict__ slot,
-    const uint64_t* __restrict__ local, const uint64_t* __restrict__ block_base,
-    rpgpu_decomp_result* __restrict__ dres, uint8_t* __restrict__ out, uint64_t out_cap,
-    rpgpu_batch_desc* __restrict__ out_descs, const uint32_t* __restrict__ scount) {
-    const uint32_t lanes = gridDim.x * blockDim.x;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += lanes) {
-        uint64_t sz = slot[i], off = 0;
-        int32_t verdict = RPGPU_V_SKIPPED;
-        uint64_t len = 0;
-        {
-            const rpgpu_batch_desc d = descs[i];
-            const rpgpu_batch_result v = vres[i];
-            const bool want = decomp_wanted(d, v);
-            // this instance's batches: its codec's lane-sized ones (+ for LZ4, the undecoded)
-            const bool mine = want ? (v.codec == CODEC && !wave_owned(d, v, sz) && scount[i] == 0) : CODEC == 3;
-            if (!mine) continue;
-            off = block_base[i / kScanBlock] + local[i];
-            if (want && plan_slot(sz, off, out_cap, verdict, len)) {
-                const uint8_t* in = data + d.offset + kHeaderSize;
-                uint8_t* o = out + off + kHeaderSize;
-                const uint64_t cap = sz - kHeaderSize - rpcodec::kSlack;
-                rpcodec::LaneEmit em;  // LZ4 blocks: lz4_block_lane
-                verdict = rpcodec::uncompress(em, CODEC, in, body_len(v), o, cap, &len);
-            }
-        }
-        finish_batch(i, reread(descs)[i], reread(vres)[i], off, sz, verdict, len, data, out, dres, out_descs);
-    }
 }
 
 // The LZ4 and snappy lane batches in one launch, one lane each, from the plan's
@@ -730,12 +700,10 @@ union ZbWs {
     rpzstd::HufWs h;
     rpzstd::SeqWs s;
 };
-// RPGPU_ZBLK_GWS 1: the entropy lanes' workspaces in the output buffer (HBM, after
-// the record region: [34..35] their offset, [36] their count), one lane per task
-// and every task at once; 0: in LDS, ~57 lanes per CU taking turns
-#ifndef RPGPU_ZBLK_GWS
-#define RPGPU_ZBLK_GWS 1
-#endif
+// The entropy lanes' workspaces live in the output buffer (HBM, after the record
+// region: [34..35] their offset, [36] their count), one lane per task and every task
+// at once.  (Round 5 kept them in LDS, ~57 lanes per CU taking turns: C5's stage 124
+// vs 63 ms beside the part kernel, profiles/r6/NOTES.md r6m.)
 constexpr uint32_t kZbGwsLanes = 65536;
 __device__ __forceinline__ bool zb_fits(const uint32_t* counter, uint64_t out_cap) {
     return cnt64(counter, 32) + (cnt64(counter, 26) + 16) * 8 <= out_cap &&
@@ -779,38 +747,6 @@ __global__ __launch_bounds__(256) void zblk_plan_kernel(
         }
     }
     frames[k] = f;
-}
-
-// E1 + E2: one lane per task (block b's sequences: task b, its literals: task
-// used + b), each lane's Huffman / FSE workspace in LDS
-__global__ __launch_bounds__(64) void zblk_entropy_kernel(
-    const rpgpu_batch_desc* __restrict__ descs, const uint8_t* __restrict__ data, const uint32_t* __restrict__ counter,
-    const uint32_t* __restrict__ wlist, const ZbFrame* __restrict__ frames, rpzstd::Blk* __restrict__ pool,
-    const uint32_t* __restrict__ bframe, uint8_t* __restrict__ out, uint64_t out_cap, uint32_t per_wg) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
-    const uint32_t l = threadIdx.x;
-    if (l >= per_wg || !zb_fits(counter, out_cap)) return;
-    ZbWs& w = reinterpret_cast<ZbWs*>(dyn_lds)[l];
-    const uint32_t used = counter[28] < counter[37] ? counter[28] : counter[37];
-    const uint64_t loff = cnt64(counter, 30), roff = cnt64(counter, 32);
-    const uint32_t lanes = gridDim.x * per_wg;
-    // tasks [0, used): the blocks' sequences (the longer ones), then [used, 2 used) their
-    // literals -- a lane's tasks alternate between the kinds whatever the grid's parity
-    for (uint32_t t = blockIdx.x * per_wg + l; t < 2 * used; t += lanes) {
-        const bool seq = t < used;
-        const uint32_t b = seq ? t : t - used, k = bframe[b];
-        if (k == ~0u) continue;
-#ifdef RPZB_DIAG_TASKS  // diagnostics build: 1 literals only, 2 sequences only (timing)
-        if ((seq ? 2 : 1) != RPZB_DIAG_TASKS) continue;
-#endif
-        const ZbFrame f = frames[k];
-        const uint8_t* in = data + descs[wlist[k]].offset + kHeaderSize;
-        const uint32_t j = b - f.first;
-        if (seq)
-            pool[b].e2 = rpzstd::blk_sequences(in, pool + f.first, j, reinterpret_cast<uint64_t*>(out + roff) + f.recs, w.s);
-        else
-            pool[b].e1 = rpzstd::blk_literals(in, pool + f.first, j, out + loff + f.lits, w.h);
-    }
 }
 
 // E1 + E2 with the workspaces in HBM: one lane per task, all of them at once
@@ -953,10 +889,10 @@ __global__ void decomp_ws_kernel(uint32_t* __restrict__ counter, uint32_t cap, u
     counter[32] = (uint32_t)br;
     counter[33] = (uint32_t)(br >> 32);
     const bool blk = counter[28] != 0;
-    // the entropy lanes' workspaces (RPGPU_ZBLK_GWS)
+    // the entropy lanes' workspaces
     const uint64_t bw = (br + (cnt64(counter, 26) + 16) * 8 + 255) & ~(uint64_t)255;
     const uint32_t used = counter[28] < counter[37] ? counter[28] : counter[37];
-    const uint32_t wl = RPGPU_ZBLK_GWS ? (2 * used < kZbGwsLanes ? 2 * used : kZbGwsLanes) : 0u;
+    const uint32_t wl = 2 * used < kZbGwsLanes ? 2 * used : kZbGwsLanes;
     counter[34] = (uint32_t)bw;
     counter[35] = (uint32_t)(bw >> 32);
     counter[36] = wl;
@@ -1035,12 +971,6 @@ __global__ __launch_bounds__(64) void decomp_wave_kernel(
 // The parts of split batches, one lane each (CODEC 3: LZ4 blocks, 2: snappy
 // chunks, 0: both); every part writes only its own output range, so they run in
 // any order.  A batch whose slot does not fit the caller's buffer decodes nothing.
-#ifndef RPGPU_PARTS_ONE_LAUNCH
-#define RPGPU_PARTS_ONE_LAUNCH 1
-#endif
-#ifndef RPGPU_PART_SPREAD
-#define RPGPU_PART_SPREAD 1
-#endif
 template <uint32_t CODEC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_WAVES))) void part_kernel(
     const SplitPart* __restrict__ parts, const uint32_t* __restrict__ pcount, uint32_t pcap,
@@ -1052,11 +982,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RPGPU_LANE_
     // first lanes; pcount = counters 4, 5 (LZ4, snappy)
     const uint32_t c3 = CODEC == 2 ? 0u : (pcount[0] < half ? pcount[0] : half);
     const uint32_t c2 = CODEC == 3 ? 0u : (pcount[CODEC == 0 ? 1 : 0] < half ? pcount[CODEC == 0 ? 1 : 0] : half);
-    // RPGPU_PART_SPREAD lanes per part (one decodes): fewer decoding lanes per wave
-    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (tid % RPGPU_PART_SPREAD) return;
-    const uint32_t lanes = gridDim.x * blockDim.x / RPGPU_PART_SPREAD;
-    for (uint32_t g = tid / RPGPU_PART_SPREAD; g < c2 + c3; g += lanes) {
+    const uint32_t lanes = gridDim.x * blockDim.x;
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < c2 + c3; g += lanes) {
         const SplitPart t = parts[g < c2 ? half + g : g - c2];
         if (t.kind == kSkipPart) continue;
         const uint64_t off = block_base[t.batch / kScanBlock] + local[t.batch];
@@ -1161,35 +1088,6 @@ __global__ void decomp_counters_kernel(uint32_t* c, uint32_t run, uint32_t pool_
 }
 
 // ------------------------------------------------------------ launchers
-// the block-parallel decoder's entropy lanes: RPGPU_ZBLK_WAVES one-wave
-// workgroups per CU share the CU's LDS, each with as many lanes as their
-// workspaces fit in its share.  The lanes decode serial chains at LDS latency:
-// spread over waves (two per SIMD) they hide each other's latency, where one
-// wave of 56 lanes per CU would not.
-#ifndef RPGPU_ZBLK_WAVES
-#define RPGPU_ZBLK_WAVES 8
-#endif
-// one ZbWs (Huffman or FSE tables) per lane
-struct ZbLaunch {
-    uint32_t grid, lanes;
-};
-ZbLaunch zblk_launch() {
-    static ZbLaunch z{0, 0};
-    if (z.grid) return z;
-    int dev = 0, cus = 0, lds = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
-    if (lds < (int)sizeof(ZbWs)) lds = (int)sizeof(ZbWs);
-    size_t k = (size_t)lds / RPGPU_ZBLK_WAVES / sizeof(ZbWs);
-    k = k > 64 ? 64 : (k < 1 ? 1 : k);
-    ZbLaunch t{(uint32_t)((cus > 0 ? cus : 256) * RPGPU_ZBLK_WAVES), (uint32_t)k};
-    hipFuncSetAttribute(reinterpret_cast<const void*>(zblk_entropy_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)(t.lanes * sizeof(ZbWs)));
-    z = t;
-    return z;
-}
-
 hipError_t launch_decomp_plan(const rpgpu_batch_desc* d_descs, uint32_t n, const uint8_t* d_data,
                               const rpgpu_batch_result* d_vres, uint64_t* d_out_bytes, void* d_scratch,
                               uint64_t max_decoded, uint32_t ws_cap, uint32_t zmode, hipStream_t s) {
@@ -1244,7 +1142,7 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     const bool zwave_any = !pc || pc[2] > (blk_fits ? pc[29] : 0u);
     const bool lzwave_any = !pc || pc[6] != 0 || parts3 || parts2;  // split fallbacks join the LZ list
     const bool zlane_any = !pc || pc[7] != 0;
-    const bool snappy_any = !pc || pc[12] != 0, gzip_any = !pc || pc[13] != 0;
+    const bool gzip_any = !pc || pc[13] != 0;
     const uint32_t nblk = (n + 255) / 256;
     decomp_counters_kernel<<<1, 64, 0, s>>>(p.counter, 1, 0);
     hipError_t e = hipGetLastError();
@@ -1301,23 +1199,13 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     // (failures join the LZ wave list).  With bodies split above 80 KiB the
     // main stream's lane launches got shorter and the snappy parts moved over
     // from the second stream, which the zstd wave decoder keeps the longer one.
-#if RPGPU_PARTS_ONE_LAUNCH
     // both codecs' parts in one launch: their lanes (C5: 43,712 + 23,765) are resident
     // at once, so the LZ4 blocks run beside the snappy chunks instead of before them
     if (parts3 || parts2) {
-        const uint32_t pgrid = (part_cap(n) < 131072u ? part_cap(n) + 255 : 131072u + 255) / 256 * RPGPU_PART_SPREAD;
+        const uint32_t pgrid = (part_cap(n) < 131072u ? part_cap(n) + 255 : 131072u + 255) / 256;
         part_kernel<0><<<pgrid, 256, 0, s>>>(p.parts, p.counter + 4, part_cap(n), d_descs, d_data, p.slot, p.local,
                                              p.block_sum, d_out, out_cap, p.pres);
     }
-#else
-    const uint32_t pgrid = (part_cap(n) / 2 < 65536u ? part_cap(n) / 2 + 255 : 65536u + 255) / 256;
-    if (parts3)
-        part_kernel<3><<<pgrid, 256, 0, s>>>(p.parts, p.counter + 4, part_cap(n), d_descs, d_data, p.slot, p.local,
-                                             p.block_sum, d_out, out_cap, p.pres);
-    if (parts2)
-        part_kernel<2><<<pgrid, 256, 0, s>>>(p.parts, p.counter + 5, part_cap(n), d_descs, d_data, p.slot, p.local,
-                                             p.block_sum, d_out, out_cap, p.pres);
-#endif
     if (ds) {
         if ((e = hipEventRecord(ds->parts, s)) != hipSuccess) return e;
     }
@@ -1332,16 +1220,10 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
             d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.counter + 1,
             p.lits, p.wlist, p.counter + 2, zb.frames, p.counter);
     if (blk_any) {
-#if RPGPU_ZBLK_GWS
         // one lane per task: pc[36] of them when the plan's counts are here, else the most
         const uint32_t wl = pc ? pc[36] : kZbGwsLanes;
         zblk_entropy_g_kernel<<<(wl + 255) / 256, 256, 0, ws>>>(d_descs, d_data, p.counter, p.wlist, zb.frames, zb.pool,
                                                                zb.bframe, d_out, out_cap);
-#else
-        const ZbLaunch zq = zblk_launch();
-        zblk_entropy_kernel<<<zq.grid, 64, zq.lanes * sizeof(ZbWs), ws>>>(d_descs, d_data, p.counter, p.wlist, zb.frames,
-                                                                       zb.pool, zb.bframe, d_out, out_cap, zq.lanes);
-#endif
         if ((e = hipGetLastError()) != hipSuccess) return e;
         zblk_exec_kernel<<<zb_frames(n), 64, 0, ws>>>(d_descs, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
                                                       out_cap, d_out_descs, p.counter, p.wlist, zb.frames, zb.pool);
@@ -1362,16 +1244,12 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                                                                   nullptr, nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t lzb = (n + 255) / 256;
-    // RPGPU_LZ_LANE_LIST 1: the LZ4 and snappy lane batches in one launch from the plan's
-    // lists (lz_lane_kernel) behind the zstd lanes on the third stream (RPGPU_LZ_LANE_MAIN
-    // 2; 1: on the main stream behind the parts, 0: on the second behind the block-parallel
+    // the LZ4 and snappy lane batches in one launch from the plan's lists
+    // (lz_lane_kernel) behind the zstd lanes on the third stream (RPGPU_LZ_LANE_MAIN 2;
+    // 1: on the main stream behind the parts, 0: on the second behind the block-parallel
     // zstd stages); the undecoded batches' verdicts on the main stream (skip_kernel).
-    // 0: one kernel
-    // per codec over every batch index (decomp_lane_kernel), as in round 5.
-#ifndef RPGPU_LZ_LANE_LIST
-#define RPGPU_LZ_LANE_LIST 1
-#endif
-#if RPGPU_LZ_LANE_LIST
+    // Round 5's kernels, one per codec over every batch index, left three lanes in
+    // four idle on a mixed arena (C5 161-164 vs 149-152 ms, profiles/r6/NOTES.md r6q).
     skip_kernel<<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, d_out_descs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (!pc || pc[12] + pc[14] != 0) {
@@ -1384,33 +1262,6 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                                                           p.wlist + 4 * (size_t)n);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
-#else
-    // RPGPU_LZ4_LANE_AUX 1: the LZ4 lanes on the second stream, behind its block-parallel
-    // zstd stages (once their entropy lanes left HBM workspaces, the shorter chain)
-#ifndef RPGPU_LZ4_LANE_AUX
-#define RPGPU_LZ4_LANE_AUX 1
-#endif
-    decomp_lane_kernel<3><<<lzb, 256, 0, RPGPU_LZ4_LANE_AUX ? ws : s>>>(d_descs, n, d_data, d_vres, p.slot, p.local,
-                                                                        p.block_sum, d_dres, d_out, out_cap,
-                                                                        d_out_descs, p.scount);
-    // the snappy lanes (second stream) start once the LZ4 lanes are done: both kernels'
-    // 1,024 workgroups want the whole GPU, and racing them for it slowed C3's LZ4 lanes
-    // (78 or 93 ms per step from run to run); in C5 the snappy lanes ran beside the zstd
-    // lanes, after the LZ4 lanes, anyway
-    if (ds && !RPGPU_LZ4_LANE_AUX) {
-        if ((e = hipEventRecord(ds->lanes, s)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(ws, ds->lanes, 0)) != hipSuccess) return e;
-    }
-    // snappy lanes on the second stream after its wave decoders (C5: the main stream
-    // carries the part kernels, the LZ4 lanes and the zstd lanes, the longer chain)
-#ifndef RPGPU_SNAPPY_LANE_AUX
-#define RPGPU_SNAPPY_LANE_AUX 1
-#endif
-    if (snappy_any)
-        decomp_lane_kernel<2><<<lzb, 256, 0, RPGPU_SNAPPY_LANE_AUX ? ws : s>>>(
-            d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, out_cap, d_out_descs, p.scount);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-#endif
 #if !RPGPU_ZSTD_LANE_STREAM
     if ((e = zlanes()) != hipSuccess) return e;
 #else
