@@ -155,11 +155,14 @@ class Engine:
         if rc != abi.RPGPU_OK:
             raise EngineError(f"rpgpu_decomp_run_device: {rc} {self.last_error()}")
 
-    def decompress_arena(self, data: np.ndarray, descs: np.ndarray, runs: int = 1) -> dict:
+    def decompress_arena(self, data: np.ndarray, descs: np.ndarray, runs: int = 1, ungated: bool = False) -> dict:
         """Validate a host arena, then decompress, rewrite and walk its compressed
         batches through the device entry points (HBM buffers from torch).
         Returns host copies: results (validation), dres, out (output buffer),
-        out_descs, out_results, index, used, out_bytes."""
+        out_descs, out_results, index, used, out_bytes.  ungated: after sizing the
+        output from a first plan, plan again and enqueue the run right behind it,
+        so the run does not find the plan's counts on the host and launches every
+        decoder (the flow of a caller that does not wait for its plan)."""
         import torch
 
         dev = torch.device("cuda", self.device)
@@ -190,6 +193,9 @@ class Engine:
         d_odescs = torch.zeros(m * 24, dtype=torch.uint8, device=dev)
         d_ores = torch.zeros(m * 64, dtype=torch.uint8, device=dev)
         d_index = torch.zeros(index_cap * 32, dtype=torch.uint8, device=dev)
+        if ungated:
+            self.decomp_plan_device(d_descs.data_ptr(), n, d_data.data_ptr(), d_res.data_ptr(),
+                                    d_used.data_ptr(), d_scr.data_ptr(), sh)
         for _ in range(runs):  # a plan may be run any number of times
             self.decomp_run_device(d_descs.data_ptr(), n, d_data.data_ptr(), d_res.data_ptr(),
                                    d_dres.data_ptr(), d_out.data_ptr(), out_cap, d_odescs.data_ptr(),

@@ -731,3 +731,25 @@ def test_zstd_block_parallel(case):
     assert (v == abi.V_OK).sum() > (len(v) // 2 if case == "mutated" else len(v) * 9 // 10)
     if case == "mutated":
         assert (v == abi.V_DECOMP_ERROR).sum() > 10
+
+
+@pytest.mark.parametrize("ungated", [False, True])
+def test_c5_shaped_arena_gated_and_ungated(eng, ungated):
+    """A C5-shaped arena (none / LZ4 / zstd / snappy-java bodies log-uniform in
+    [7 B, 1 MiB], 1 % corruption) against the oracle, with the run reading the
+    plan's counts on the host (the broker's flow: only the decoders with work
+    are launched) and enqueued right behind a fresh plan (every decoder
+    launched, the counts read on the device): the split parts, the listed LZ
+    lanes, the zstd lanes, the block-parallel zstd stages with their HBM
+    workspaces and the wave decoders, on the context's three streams."""
+    from redpanda_amd import abi, engine
+
+    mix = (1 << 0) | (1 << 2) | (1 << 3) | (1 << 4)
+    spec = engine.make_spec(seed=0x5EED0C55, partitions=64, records_per_batch=1, key_len=0, value_len=0,
+                            codec_mix=mix, body_min=7, body_max=1 << 20, corrupt_ppm=10_000, corrupt_mask=0x3FF,
+                            ops=abi.OPS_PRODUCE | abi.OP_DECOMP, payload=abi.PAYLOAD_TEXT)
+    data, descs = engine.build_arena(spec, 1500, nthreads=8)
+    got = eng.decompress_arena(data, descs, runs=2, ungated=ungated)
+    want = compare(got, data, descs, nthreads=8)
+    v = want["verdicts"]
+    assert (v == abi.V_OK).sum() > 1000
