@@ -1147,6 +1147,11 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
     decomp_counters_kernel<<<1, 64, 0, s>>>(p.counter, 1, 0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    // the verdicts of the batches nothing decodes, first: behind the decoders it waited
+    // for CUs the zstd lanes' 256-VGPR waves held (C4: a 313 ms span for microseconds of work)
+    skip_kernel<<<(n + 255) / 256, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out,
+                                               d_out_descs);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     // large batches on the wave decoders, on a second stream beside the lanes;
     // the zstd / gzip lane decoders on a third (RPGPU_ZSTD_LANE_STREAM 0: on the
     // main stream after the LZ4 / snappy lanes, as before round 5)
@@ -1243,15 +1248,12 @@ hipError_t launch_decomp_run(const rpgpu_batch_desc* d_descs, uint32_t n, const 
                                                                   p.counter, p.lits, p.wlist + n, p.counter + 3,
                                                                   nullptr, nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const uint32_t lzb = (n + 255) / 256;
     // the LZ4 and snappy lane batches in one launch from the plan's lists
     // (lz_lane_kernel) behind the zstd lanes on the third stream (RPGPU_LZ_LANE_MAIN 2;
     // 1: on the main stream behind the parts, 0: on the second behind the block-parallel
-    // zstd stages); the undecoded batches' verdicts on the main stream (skip_kernel).
+    // zstd stages); the undecoded batches' verdicts come first (skip_kernel, above).
     // Round 5's kernels, one per codec over every batch index, left three lanes in
     // four idle on a mixed arena (C5 161-164 vs 149-152 ms, profiles/r6/NOTES.md r6q).
-    skip_kernel<<<lzb, 256, 0, s>>>(d_descs, n, d_data, d_vres, p.slot, p.local, p.block_sum, d_dres, d_out, d_out_descs);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     if (!pc || pc[12] + pc[14] != 0) {
         const uint32_t cnt = pc ? pc[12] + pc[14] : n;
 #ifndef RPGPU_LZ_LANE_MAIN
