@@ -89,6 +89,11 @@ CONFIGS = {
                  "uncovered-field flips, truncation, re-CRC'd malformed records, corrupt compressed "
                  "payloads, codec bits 5..7), 65,536 partitions; validate + decompress + rewrite + walk",
         batches=1 << 17, partitions=65536, decompress=True, cpu_sample=2048,
+        # rpgpu_opts.walk_chunks: the input's checksum / walk overlap in 8 chunks, not 16 --
+        # with batches from 7 B to 1 MiB each chunk waits for its largest ones
+        # (C5 123.3-123.9 -> 118.6 ms per step; 1 / 2 / 4 chunks 120.3 / 122.7 / 119.8,
+        # profiles/r6/NOTES.md r6cc)
+        walk_chunks=8,
         spec=dict(records_per_batch=1, key_len=0, value_len=0, codec_mix=C5_MIX, body_min=7,
                   body_max=1 << 20, corrupt_ppm=10_000, corrupt_mask=0x3FF)),
 }
@@ -443,7 +448,7 @@ def main() -> int:
     # of serial validate-then-walk, C2 ~9 % faster; profiles/r4/NOTES.md r4i / r4j)
     overlap = args.overlap != "off"
     eng = engine.Engine(local, walk_overlap=overlap, decomp_ws_lanes=args.ws_lanes or cfg.get("ws_lanes", 0),
-                        walk_chunks=args.walk_chunks, blocks_per_cu=args.blocks_per_cu,
+                        walk_chunks=args.walk_chunks or cfg.get("walk_chunks", 0), blocks_per_cu=args.blocks_per_cu,
                         zstd_blocks=args.zstd_blocks == "on")
     chunks, P_total, part_shift, (plo, phi) = rank_chunks(cfg, rank, world, scaling, args.batches)
     n = sum(m for _, m in chunks)
@@ -629,6 +634,9 @@ def main() -> int:
                      "algorithmic_bytes_per_launch": int(alg_bytes)},
         "cpu_baseline": None,
     }
+    wc = args.walk_chunks or cfg.get("walk_chunks", 0)
+    if wc:
+        out["config"]["walk_chunks"] = wc  # rpgpu_opts.walk_chunks (0 / absent: the library's 16)
     if decompress:
         out["config"]["payload"] = args.payload
         out["config"]["decompressed_bytes_per_batch_avg"] = round(dec / max(n, 1), 1)
